@@ -1,0 +1,13 @@
+"""MI355X-native QGMAP optical flow (drop-in for gqmap_gpu_mixture.m /
+gqmap_gpuSuper_mix_entropy.m).  The compute lives in libgqmap.so (HIP,
+gfx950); this package is the host-side mirror of the reference's call
+interface and driver scripts."""
+from .engine import (Engine, State, aepe, gqmap_gpu_mixture, gqmap_gpuSuper_mix_entropy,
+                     initial_state, make_options, rand_uniform)
+from .flowio import load_pair, read_flow_file, rgb2gray, write_flow_file
+from .ops import flow_to_color, gauss_hermite, mixture_map, projsplx
+
+__all__ = ["Engine", "State", "aepe", "gqmap_gpu_mixture", "gqmap_gpuSuper_mix_entropy",
+           "initial_state", "make_options", "rand_uniform", "load_pair", "read_flow_file",
+           "rgb2gray", "write_flow_file", "flow_to_color", "gauss_hermite", "mixture_map",
+           "projsplx"]

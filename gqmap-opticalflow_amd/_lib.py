@@ -1,0 +1,128 @@
+"""ctypes binding of libgqmap.so (include/gqmap.h).
+
+The shared library is the product: HIP kernels for gfx950 plus the host
+runtime.  This module never falls back to anything else -- if the library is
+missing or no GPU is present the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libgqmap.so")
+
+GQMAP_OK = 0
+ENGINE_MIXTURE, ENGINE_SUPER = 0, 1
+FP64, FP32 = 0, 1
+ALPHA_SOFTMAX, ALPHA_PROJSPLX = 0, 1
+LMAX, KMAX = 8, 16
+
+# Every entry point declared in include/gqmap.h (checked by tests/test_abi.py).
+EXPORTS = (
+    "gqmap_options_default", "gqmap_create", "gqmap_set_images", "gqmap_init_state",
+    "gqmap_set_state", "gqmap_get_state", "gqmap_run", "gqmap_run_timed", "gqmap_get_info",
+    "gqmap_get_map", "gqmap_log_p", "gqmap_synchronize", "gqmap_destroy", "gqmap_projsplx",
+    "gqmap_mixture_map", "gqmap_flow_to_color", "gqmap_gauss_hermite", "gqmap_rand_uniform",
+    "gqmap_last_error", "gqmap_abi_version", "gqmap_device_count",
+)
+
+
+class GqmapOptions(C.Structure):
+    _fields_ = [
+        ("its", C.c_int), ("K", C.c_int), ("L", C.c_int),
+        ("temperature", C.c_double), ("drate", C.c_double), ("epsn", C.c_double),
+        ("lambdad", C.c_double), ("lambdas", C.c_double),
+        ("minu", C.c_double), ("maxu", C.c_double), ("minv", C.c_double), ("maxv", C.c_double),
+        ("engine", C.c_int), ("precision", C.c_int), ("alpha_mode", C.c_int),
+        ("alpha_start", C.c_int), ("alpha_lr", C.c_double),
+        ("guard_a", C.c_int), ("t_decay_every", C.c_int), ("t_min", C.c_double),
+        ("step0", C.c_double), ("step_decay", C.c_double),
+        ("sig_lo", C.c_double), ("sig_hi", C.c_double), ("corr_tor", C.c_double),
+        ("tor", C.c_double),
+    ]
+
+
+_D = C.POINTER(C.c_double)
+
+
+class GqmapState(C.Structure):
+    _fields_ = [("muu", _D), ("muv", _D), ("sigu", _D), ("sigv", _D), ("pn", _D),
+                ("rou", _D), ("w", _D), ("alpha", _D), ("it", C.c_int), ("T", C.c_double)]
+
+
+class GqmapInfo(C.Structure):
+    _fields_ = [("Mo", C.c_int), ("No", C.c_int), ("M", C.c_int), ("N", C.c_int),
+                ("L", C.c_int), ("K", C.c_int), ("it", C.c_int), ("stopped", C.c_int),
+                ("T", C.c_double), ("device", C.c_int)]
+
+
+class GqmapError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libgqmap.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GqmapError(f"{LIB_PATH} not built: run `make -C {PKG_DIR}` "
+                         "(or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    u8 = P(C.c_uint8)
+    vp = C.c_void_p
+    sig = {
+        "gqmap_options_default": (None, [P(GqmapOptions), C.c_int]),
+        "gqmap_create": (C.c_int, [P(vp), P(GqmapOptions), C.c_int]),
+        "gqmap_set_images": (C.c_int, [vp, _D, _D, C.c_int, C.c_int]),
+        "gqmap_init_state": (C.c_int, [vp, C.c_uint64]),
+        "gqmap_set_state": (C.c_int, [vp, P(GqmapState)]),
+        "gqmap_get_state": (C.c_int, [vp, P(GqmapState)]),
+        "gqmap_run": (C.c_int, [vp, C.c_int, P(C.c_int), _D]),
+        "gqmap_run_timed": (C.c_int, [vp, C.c_int, P(C.c_int), _D, _D]),
+        "gqmap_get_info": (C.c_int, [vp, P(GqmapInfo)]),
+        "gqmap_get_map": (C.c_int, [vp, _D]),
+        "gqmap_log_p": (C.c_int, [vp, _D, _D]),
+        "gqmap_synchronize": (C.c_int, [vp]),
+        "gqmap_destroy": (None, [vp]),
+        "gqmap_projsplx": (C.c_int, [_D, _D, C.c_int, C.c_int, C.c_int]),
+        "gqmap_mixture_map": (C.c_int, [_D, _D, _D, _D, _D, C.c_int, C.c_int, C.c_int, _D, C.c_int]),
+        "gqmap_flow_to_color": (C.c_int, [_D, C.c_int, C.c_int, C.c_double, u8, _D, _D, u8, C.c_int]),
+        "gqmap_gauss_hermite": (C.c_int, [C.c_int, _D, _D]),
+        "gqmap_rand_uniform": (None, [C.c_uint64, C.c_uint32, C.c_uint64, C.c_size_t, _D]),
+        "gqmap_last_error": (C.c_char_p, []),
+        "gqmap_abi_version": (C.c_int, []),
+        "gqmap_device_count": (C.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str = "gqmap") -> None:
+    if status != GQMAP_OK:
+        msg = load().gqmap_last_error().decode(errors="replace")
+        raise GqmapError(f"{what}: status {status}: {msg}")
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(_D)
+
+
+def u8ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def f64(a) -> np.ndarray:
+    """Column-major contiguous float64 view/copy (MATLAB layout)."""
+    return np.require(np.asarray(a, dtype=np.float64), requirements=["F_CONTIGUOUS", "ALIGNED"])

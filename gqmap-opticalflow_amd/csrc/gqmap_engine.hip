@@ -1,0 +1,1189 @@
+// gqmap_engine.hip -- the QGMAP iteration on CDNA4 (gfx950).
+//
+// One iteration of gqmap_gpu_mixture.m:27-75 (and gqmap_gpuSuper_mix_entropy.m:26-75)
+// is two launches:
+//
+//   k_iter      fused stencil kernel: node potentials + node gradient
+//               (node_grad_spectral, :87-116), the four owned edges
+//               (edge_grad_spectral, :118-146), the 1-px halo edges recomputed
+//               into LDS, the neighbour gradient scatter (:37-40), the clamped
+//               ascent (:41-46) and per-workgroup partial sums of Energy,
+//               dalpha, |dmu|, |dsigma| (:36, :48, :69-70).  Jacobi update:
+//               reads state buffer A, writes buffer B (ping-pong).
+//   k_finalize  one workgroup: deterministic reduction of the partials, the
+//               alpha update (softmax :78-86 or projsplx :49), the temperature
+//               decay (super :72), the stop test (:75), the trace record.
+//
+// All loop control lives on the device (Ctl), so a chunk of iterations is
+// captured once into a hipGraph and replayed; a stopped run turns the
+// remaining launches into no-ops.
+//
+// Layout: every field is a MATLAB column-major plane (m fastest).  A state
+// buffer is 9 planes of M*N*L: muu, muv, sigu, sigv, pn, rou(dir=1,u),
+// rou(dir=2,u), rou(dir=1,v), rou(dir=2,v) -- i.e. rou(m,n,l,dir,uv) exactly as
+// the reference's 5-D array.  Tiles of 16x16 nodes map to 256-thread
+// workgroups (4 wave64s); lane order is m-fastest so state loads coalesce.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gqmap_internal.h"
+
+namespace gq {
+
+constexpr int TILE = 16;
+constexpr int BLOCK = TILE * TILE;
+constexpr int TS = 256;        // quadrature table stride (K2 <= 256)
+constexpr int NTAB = 8;        // xi, xj, w, w*xi, w*xj, w*(xi^2+xj^2), w*(xi^2-xj^2), w*xi*xj
+constexpr int NPLANES = 9;
+constexpr int TRACE_CAP = 8192;
+constexpr int GRAPH_CHUNK = 50;
+
+struct Ctl {
+    int it;    // next iteration (1-based)
+    int done;  // completed iterations since the state was set (ping-pong parity)
+    int stop;  // ptdmu < tor reached
+    int pad;
+    double T;
+    double alpha[GQMAP_LMAX];
+    double w[GQMAP_LMAX];
+};
+
+template <typename R>
+struct IterParams {
+    const R *__restrict__ VV;   // (Mo+2) x (No+2) cubic-convolution padded I2
+    const R *__restrict__ I1;   // Mo x No
+    R *st0;
+    R *st1;
+    const R *__restrict__ tab;  // NTAB x TS
+    Ctl *ctl;
+    double *partials;           // nblocks x (3 + L)
+    int M, N, Mo, No, M2, L, K2;
+    int tiles_m, tiles_n;
+    R epsn, lamd, lams;
+    R minu, maxu, minv, maxv, sig_lo, sig_hi, corr;
+    double step0, step_decay;
+    int guard;
+    int64_t MNL;
+};
+
+// ---------------------------------------------------------------------------
+// device math
+// ---------------------------------------------------------------------------
+template <typename R>
+__device__ __forceinline__ void keys4(R t, R &w0, R &w1, R &w2, R &w3)
+{
+    // Keys a=-1/2 weights in the x2 form of node_pot (gqmap_gpu_mixture.m:167-174)
+    w0 = ((R(2) - t) * t - R(1)) * t;
+    w1 = (R(3) * t - R(5)) * t * t + R(2);
+    w2 = ((R(4) - R(3) * t) * t + R(1)) * t;
+    w3 = (t - R(1)) * t * t;
+}
+
+template <typename R>
+__device__ __forceinline__ R bicubic_cell(const R *__restrict__ c, int M2, R so, R to)
+{
+    R t0, t1, t2, t3, s0, s1, s2, s3;
+    keys4(to, t0, t1, t2, t3);
+    keys4(so, s0, s1, s2, s3);
+    const R v0 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
+    c += M2;
+    const R v1 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
+    c += M2;
+    const R v2 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
+    c += M2;
+    const R v3 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
+    return (s0 * v0 + s1 * v1 + s2 * v2 + s3 * v3) * R(0.25);
+}
+
+// interp2-cubic sample at 1-based column jj + x1, row ii + x2 (node_pot, :157-176).
+// fp64 mirrors the reference arithmetic (Xq = j + x1, clamp, floor).
+__device__ __forceinline__ double sample(const double *__restrict__ VV, int M2, int Mo, int No,
+                                         int ii, int jj, double x1, double x2)
+{
+    const double Xq = fmin(fmax(jj + x1, 1.0), (double)No);
+    const double Yq = fmin(fmax(ii + x2, 1.0), (double)Mo);
+    const int ix = min((int)Xq, No - 1);  // Xq >= 1: truncation == floor
+    const int iy = min((int)Yq, Mo - 1);
+    return bicubic_cell(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, Xq - ix, Yq - iy);
+}
+// fp32: split the offset into integer + fraction relative to the pixel so the
+// fractional position keeps full precision at any image size.
+__device__ __forceinline__ float sample(const float *__restrict__ VV, int M2, int Mo, int No,
+                                        int ii, int jj, float x1, float x2)
+{
+    x1 = fminf(fmaxf(x1, float(1 - jj)), float(No - jj));
+    x2 = fminf(fmaxf(x2, float(1 - ii)), float(Mo - ii));
+    const float fx = floorf(x1), fy = floorf(x2);
+    float so = x1 - fx, to = x2 - fy;
+    int ix = jj + (int)fx, iy = ii + (int)fy;
+    if (ix > No - 1) { ix = No - 1; so = 1.f; }
+    if (iy > Mo - 1) { iy = Mo - 1; to = 1.f; }
+    return bicubic_cell(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, so, to);
+}
+
+// sqrt for arguments in [1e-300, 1e300] (every call site passes eps + d^2 or
+// 1 +- p with eps > 0, |p| < 1): the same rsq + Goldschmidt + two Newton
+// corrections LLVM emits for sqrt(double), minus its denormal rescaling.
+__device__ __forceinline__ double dsqrt(double x)
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+__device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double dlog(double x) { return log(x); }
+__device__ __forceinline__ float dlog(float x) { return __logf(x); }
+
+// Quadrature tables are read with wave-uniform indices; routing them through
+// the constant address space turns every access into a scalar (SMEM) load.
+template <typename R>
+using ctab_t = const __attribute__((address_space(4))) R *;
+template <typename R>
+__device__ __forceinline__ ctab_t<R> as_const(const R *p)
+{
+    return (ctab_t<R>)p;
+}
+
+template <typename R>
+struct Grad {
+    R da, du1, du2, do1, do2, dp, E;
+};
+
+// Basis sums of the quadrature: with f_k = WIWJ(k)*pot_k,
+//   S0=sum f, Sxi=sum f*XI, Sxj=sum f*XJ, Sa=sum f*(XI^2+XJ^2), Sm=sum f*(XI^2-XJ^2), Sx=sum f*XI*XJ
+// every accumulator of the reference (dp, du1, du2, do1, do2, Ei) is a fixed
+// linear combination of these six (gqmap_gpu_mixture.m:99-105).
+template <typename R>
+struct Sums {
+    R s0 = 0, sxi = 0, sxj = 0, sa = 0, sm = 0, sx = 0;
+    __device__ __forceinline__ void add(ctab_t<R> tab, int k, R f)
+    {
+        s0 = fma(tab[2 * TS + k], f, s0);
+        sxi = fma(tab[3 * TS + k], f, sxi);
+        sxj = fma(tab[4 * TS + k], f, sxj);
+        sa = fma(tab[5 * TS + k], f, sa);
+        sm = fma(tab[6 * TS + k], f, sm);
+        sx = fma(tab[7 * TS + k], f, sx);
+    }
+};
+
+// Epilogue shared by node (tau = -3T) and edge (tau = +T) gradients
+// (gqmap_gpu_mixture.m:107-115 and :137-145).  `lam` = -lambda (potential scale).
+template <typename R>
+__device__ __forceinline__ Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s,
+                                            R t, R tau, bool live)
+{
+    const R pi = R(M_PI), c1 = R(2.8378770664093454835606594728112);  // 1+log(2*pi)
+    const R S0 = lam * S.s0, Sxi = lam * S.sxi, Sxj = lam * S.sxj;
+    const R Sa = lam * S.sa, Sm = lam * S.sm, Sx = lam * S.sx;
+    const R pr = R(1) - p * p, sqrtpr = dsqrt(pr);
+    R dp = p * S0 - p * Sa + R(2) * Sx;
+    R du1 = (s - p * t) * Sxi + (t - p * s) * Sxj;
+    R du2 = (t - p * s) * Sxi + (s - p * t) * Sxj;
+    R do1 = Sa - S0 + Sm / sqrtpr;
+    R do2 = Sa - S0 - Sm / sqrtpr;
+    if (!live) dp = du1 = du2 = do1 = do2 = R(0);
+    Grad<R> g;
+    const R sq2 = R(M_SQRT2);
+    g.du1 = a * du1 * (sq2 / (o1 * pr)) / pi;
+    g.du2 = a * du2 * (sq2 / (o2 * pr)) / pi;
+    const R ent = tau != R(0) ? tau * (c1 + dlog(sqrtpr * o1 * o2)) : R(0);
+    g.da = S0 / pi + ent;
+    g.do1 = a * (do1 / pi + tau) / o1;
+    g.do2 = a * (do2 / pi + tau) / o2;
+    g.dp = a * (dp / pi - tau * p) / pr;
+    g.E = a * g.da;
+    return g;
+}
+
+template <typename R>
+__device__ __forceinline__ void spectral_st(R p, R &s, R &t)
+{
+    const R sp = dsqrt(R(1) + p), sm = dsqrt(R(1) - p);
+    s = (sp + sm) * R(0.5);
+    t = (sp - sm) * R(0.5);
+}
+
+// edge_grad_spectral (gqmap_gpu_mixture.m:118-146) with edge_pot (:180-182)
+template <typename R>
+__device__ __forceinline__ Grad<R> edge_grad(const IterParams<R> &P, R T, R a, R u1, R u2, R o1,
+                                             R o2, R p)
+{
+    R s, t;
+    spectral_st(p, s, t);
+    const R sq2 = R(M_SQRT2);
+    // x1 - x2 = sq2*o1*(s XI + t XJ) + u1 - sq2*o2*(t XI + s XJ) - u2
+    const R A = sq2 * (o1 * s - o2 * t), B = sq2 * (o1 * t - o2 * s), C = u1 - u2;
+    Sums<R> S;
+    const ctab_t<R> tab = as_const(P.tab);
+    const R eps = P.epsn;
+#pragma unroll 2
+    for (int k = 0; k < P.K2; ++k) {
+        const R d = fma(A, tab[k], fma(B, tab[TS + k], C));
+        S.add(tab, k, dsqrt(fma(d, d, eps)));
+    }
+    return epilogue(S, -P.lams, a, o1, o2, p, s, t, T, !P.guard || a != R(0));
+}
+
+// node_grad_spectral (gqmap_gpu_mixture.m:87-116; super: gqmap_gpuSuper_mix_entropy.m:87-122)
+template <typename R, bool SUPER>
+__device__ __forceinline__ Grad<R> node_grad(const IterParams<R> &P, R T, R a, R u1, R u2, R o1,
+                                             R o2, R p, int m, int n)
+{
+    R s, t;
+    spectral_st(p, s, t);
+    const R sq2 = R(M_SQRT2);
+    const R ax = sq2 * o1 * s, bx = sq2 * o1 * t;  // x1 = ax*XI + bx*XJ + u1
+    const R ay = sq2 * o2 * t, by = sq2 * o2 * s;  // x2 = ay*XI + by*XJ + u2
+    Sums<R> S;
+    const ctab_t<R> tab = as_const(P.tab);
+    const R eps = P.epsn;
+    if constexpr (!SUPER) {
+        const R I = P.I1[m + (int64_t)P.Mo * n];
+#pragma unroll 1
+        for (int k = 0; k < P.K2; ++k) {
+            const R x1 = fma(ax, tab[k], fma(bx, tab[TS + k], u1));
+            const R x2 = fma(ay, tab[k], fma(by, tab[TS + k], u2));
+            const R d = I - sample(P.VV, P.M2, P.Mo, P.No, m + 1, n + 1, x1, x2);
+            S.add(tab, k, dsqrt(fma(d, d, eps)));
+        }
+    } else {
+        R I[16];
+        const int i0 = 4 * m, j0 = 4 * n;  // 0-based top-left pixel of the 4x4 block
+#pragma unroll
+        for (int q = 0; q < 16; ++q) I[q] = P.I1[(i0 + (q & 3)) + (int64_t)P.Mo * (j0 + (q >> 2))];
+#pragma unroll 1
+        for (int k = 0; k < P.K2; ++k) {
+            const R x1 = fma(ax, tab[k], fma(bx, tab[TS + k], u1));
+            const R x2 = fma(ay, tab[k], fma(by, tab[TS + k], u2));
+            R f = 0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const R d = I[q] - sample(P.VV, P.M2, P.Mo, P.No, i0 + (q & 3) + 1,
+                                          j0 + (q >> 2) + 1, x1, x2);
+                f += dsqrt(fma(d, d, eps));
+            }
+            S.add(tab, k, f);
+        }
+    }
+    return epilogue(S, -P.lamd, a, o1, o2, p, s, t, R(-3) * T, !P.guard || a != R(0));
+}
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// fused iteration kernel
+// ---------------------------------------------------------------------------
+template <typename R, bool SUPER>
+__global__ __launch_bounds__(BLOCK) void k_iter(IterParams<R> P)
+{
+    const Ctl *ctl = P.ctl;
+    if (ctl->stop) return;
+    const int it = ctl->it;
+    const int parity = ctl->done & 1;
+    const R *__restrict__ src = parity ? P.st1 : P.st0;
+    R *__restrict__ dst = parity ? P.st0 : P.st1;
+    const R T = R(ctl->T);
+    const R step = R(P.step0 / (1.0 + it / P.step_decay));
+
+    // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin
+    // dispatch), so give each XCD a contiguous band of tiles (L2 locality of
+    // the VV gathers).  Speed only; correctness never depends on placement.
+    const int nb = P.tiles_m * P.tiles_n;
+    const int b = blockIdx.x;
+    int tile = b >> 3;
+    {
+        const int xcd = b & 7;
+        for (int y = 0; y < xcd; ++y) tile += (nb - y + 7) >> 3;  // blocks owned by XCD groups < xcd
+    }
+    const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
+    const int tid = threadIdx.x;
+    const int lm = tid & (TILE - 1), ln = tid >> 4;
+    const int m0 = tm * TILE, n0 = tn * TILE;
+    const int m = m0 + lm, n = n0 + ln;
+    const int M = P.M, N = P.N;
+    const int64_t MNL = P.MNL;
+    const bool valid = m < M && n < N;
+    auto interior = [&](int mm, int nn) { return mm >= 1 && mm <= M - 2 && nn >= 1 && nn <= N - 2; };
+    const bool inner = valid && interior(m, n);
+
+    // in_up[uv][q][ln][lm]: du2/do2 of the edge from (m-1,n); in_left: from (m,n-1)
+    __shared__ R in_up[2][2][BLOCK];
+    __shared__ R in_left[2][2][BLOCK];
+    __shared__ double red[4][8];
+
+    double acc_E = 0, acc_mu = 0, acc_sg = 0;
+    double acc_da[GQMAP_LMAX];
+#pragma unroll
+    for (int l = 0; l < GQMAP_LMAX; ++l) acc_da[l] = 0;
+
+    for (int l = 0; l < P.L; ++l) {
+        const R a = R(ctl->alpha[l]);
+        const int64_t i = m + (int64_t)M * n + MNL * l;
+        R own[NPLANES];
+#pragma unroll
+        for (int q = 0; q < NPLANES; ++q) own[q] = valid ? src[i + MNL * q] : R(0);
+        Grad<R> nd{};
+        if (inner) nd = node_grad<R, SUPER>(P, T, a, own[0], own[1], own[2], own[3], own[4], m, n);
+        // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
+        // edges, then job 4: wave 0 recomputes the 64 halo edges entering
+        // the tile from the row above / the column to the left.  One edge
+        // body, streamed into accumulators and LDS, keeps VGPRs low.
+        R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1/do1
+        R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
+        double eacc = 0, dacc = 0;
+        const int njobs = tid < 64 ? 5 : 4;  // wave-uniform
+#pragma unroll 1
+        for (int e = 0; e < njobs; ++e) {
+            int dir, uv, hm, hn, rm, rn;
+            bool own_edge = e < 4;
+            if (own_edge) {
+                dir = e & 1; uv = e >> 1;
+                hm = m; hn = n;
+                rm = dir == 0 ? m + 1 : m; rn = dir == 1 ? n + 1 : n;
+            } else {
+                const bool top = tid < 32;
+                uv = (tid >> 4) & 1;
+                const int r = tid & 15;
+                dir = top ? 0 : 1;
+                hm = top ? m0 - 1 : m0 + r; hn = top ? n0 + r : n0 - 1;
+                rm = top ? m0 : hm;         rn = top ? hn : n0;
+            }
+            const bool r_inner = rm < M && rn < N && interior(rm, rn);
+            const bool need = own_edge ? (inner || (valid && r_inner))
+                                       : (hm >= 0 && hn >= 0 && r_inner);
+            Grad<R> g{};
+            if (need) {
+                const int64_t h = hm + (int64_t)M * hn + MNL * l;
+                const int64_t r = rm + (int64_t)M * rn + MNL * l;
+                const R u1 = own_edge ? (uv ? own[1] : own[0]) : src[h + MNL * uv];
+                const R o1 = own_edge ? (uv ? own[3] : own[2]) : src[h + MNL * (2 + uv)];
+                const R p = own_edge ? (e == 0 ? own[5] : e == 1 ? own[6] : e == 2 ? own[7] : own[8])
+                                     : src[h + MNL * (5 + dir + 2 * uv)];
+                g = edge_grad(P, T, a, u1, src[r + MNL * uv], o1, src[r + MNL * (2 + uv)], p);
+            }
+            if (own_edge) {
+                if (uv == 0) { sum_mu0 += g.du1; sum_sg0 += g.do1; }
+                else         { sum_mu1 += g.du1; sum_sg1 += g.do1; }
+                if (e == 0) drou0 = g.dp; else if (e == 1) drou1 = g.dp;
+                else if (e == 2) drou2 = g.dp; else drou3 = g.dp;
+                eacc += (double)g.E;
+                dacc += (double)g.da;
+                // neighbour share: (m+1,n) reads in_up, (m,n+1) reads in_left
+                if (dir == 0 && lm + 1 < TILE) { in_up[uv][0][tid + 1] = g.du2; in_up[uv][1][tid + 1] = g.do2; }
+                if (dir == 1 && ln + 1 < TILE) { in_left[uv][0][tid + TILE] = g.du2; in_left[uv][1][tid + TILE] = g.do2; }
+            } else {
+                const int r = tid & 15;
+                if (dir == 0) { in_up[uv][0][r * TILE] = g.du2; in_up[uv][1][r * TILE] = g.do2; }
+                else          { in_left[uv][0][r] = g.du2; in_left[uv][1][r] = g.do2; }
+            }
+        }
+        __syncthreads();
+        if (inner) {
+            // dmuu = dmuu + sum(dmu1(:,:,:,:,1),4) + circshift(dmu2(..1,1),1) + circshift(dmu2(..2,1),1,2)
+            const R gmu_u = nd.du1 + sum_mu0 + in_up[0][0][tid] + in_left[0][0][tid];
+            const R gmu_v = nd.du2 + sum_mu1 + in_up[1][0][tid] + in_left[1][0][tid];
+            const R gsg_u = nd.do1 + sum_sg0 + in_up[0][1][tid] + in_left[0][1][tid];
+            const R gsg_v = nd.do2 + sum_sg1 + in_up[1][1][tid] + in_left[1][1][tid];
+            auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
+            dst[i + MNL * 0] = cl(own[0] + gmu_u * step, P.minu, P.maxu);
+            dst[i + MNL * 1] = cl(own[1] + gmu_v * step, P.minv, P.maxv);
+            dst[i + MNL * 2] = cl(own[2] + gsg_u * step, P.sig_lo, P.sig_hi);
+            dst[i + MNL * 3] = cl(own[3] + gsg_v * step, P.sig_lo, P.sig_hi);
+            dst[i + MNL * 4] = cl(own[4] + nd.dp * step, -P.corr, P.corr);
+            dst[i + MNL * 5] = cl(own[5] + drou0 * step, -P.corr, P.corr);
+            dst[i + MNL * 6] = cl(own[6] + drou1 * step, -P.corr, P.corr);
+            dst[i + MNL * 7] = cl(own[7] + drou2 * step, -P.corr, P.corr);
+            dst[i + MNL * 8] = cl(own[8] + drou3 * step, -P.corr, P.corr);
+            acc_E += (double)nd.E + eacc;
+            const double dal = (double)nd.da + dacc;
+#pragma unroll
+            for (int q = 0; q < GQMAP_LMAX; ++q)
+                if (q == l) acc_da[q] += dal;
+            acc_mu += fabs((double)gmu_u);
+            acc_sg += fabs((double)gsg_u);
+        }
+        __syncthreads();  // LDS reuse by the next component
+    }
+
+    // block partials: Energy, sum|dmu_u|, sum|dsigma_u|, dalpha[0..L-1]
+    const int NP = 3 + P.L;
+    const int wave = tid >> 6, lane = tid & 63;
+    double* out = P.partials + (int64_t)blockIdx.x * NP;
+    for (int q = 0; q < NP; ++q) {
+        double v = q == 0 ? acc_E : q == 1 ? acc_mu : q == 2 ? acc_sg : 0.0;
+#pragma unroll
+        for (int l = 0; l < GQMAP_LMAX; ++l)
+            if (q == 3 + l) v = acc_da[l];
+        v = wave_sum(v);
+        if (lane == 0) red[wave][q & 7] = v;
+        __syncthreads();
+        if (tid == 0) out[q] = (red[0][q & 7] + red[1][q & 7]) + (red[2][q & 7] + red[3][q & 7]);
+        __syncthreads();
+    }
+}
+
+struct FinParams {
+    const double *partials;
+    int nblocks, L;
+    Ctl *ctl;
+    double *trace;     // TRACE_CAP x 3
+    double count;      // interior nodes * L
+    double step0, step_decay;
+    int alpha_mode, alpha_start;
+    double alpha_lr;
+    int t_decay_every;
+    double drate, t_min, tor;
+};
+
+__global__ __launch_bounds__(256) void k_finalize(FinParams F)
+{
+    Ctl *ctl = F.ctl;
+    if (ctl->stop) return;
+    __shared__ double sh[256];
+    __shared__ double tot[3 + GQMAP_LMAX];
+    const int NP = 3 + F.L;
+    const int tid = threadIdx.x;
+    for (int q = 0; q < NP; ++q) {
+        double v = 0;
+        for (int b = tid; b < F.nblocks; b += 256) v += F.partials[(int64_t)b * NP + q];
+        sh[tid] = v;
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if (tid < s) sh[tid] += sh[tid + s];
+            __syncthreads();
+        }
+        if (tid == 0) tot[q] = sh[0];
+        __syncthreads();
+    }
+    if (tid != 0) return;
+    const int it = ctl->it;
+    const double step = F.step0 / (1.0 + it / F.step_decay);
+    const double energy = tot[0], ptdmu = tot[1] / F.count, ptdsig = tot[2] / F.count;
+    const int L = F.L;
+    if (it > F.alpha_start && L != 1) {
+        if (F.alpha_mode == GQMAP_ALPHA_SOFTMAX) {  // updateAlpha, gqmap_gpu_mixture.m:78-86
+            double sda = 0;
+            for (int l = 0; l < L; ++l) sda += tot[3 + l] * ctl->alpha[l];
+            double se = 0, ew[GQMAP_LMAX];
+            for (int l = 0; l < L; ++l) {
+                const double dw = ctl->alpha[l] * (tot[3 + l] - sda);
+                ctl->w[l] = fmin(fmax(ctl->w[l] + dw * step * F.alpha_lr, -300.0), 300.0);
+                ew[l] = exp(ctl->w[l]);
+                se += ew[l];
+            }
+            for (int l = 0; l < L; ++l) ctl->alpha[l] = ew[l] / se;
+        } else {  // projsplx(alpha + dalpha*step*lr), projsplx.m:15-30
+            double y[GQMAP_LMAX], s[GQMAP_LMAX];
+            for (int l = 0; l < L; ++l) s[l] = y[l] = ctl->alpha[l] + tot[3 + l] * step * F.alpha_lr;
+            for (int i = 1; i < L; ++i) {
+                double v = s[i];
+                int j = i;
+                while (j > 0 && s[j - 1] < v) { s[j] = s[j - 1]; --j; }
+                s[j] = v;
+            }
+            double tmpsum = 0, tmax = 0;
+            bool bget = false;
+            for (int ii = 0; ii < L - 1; ++ii) {
+                tmpsum += s[ii];
+                tmax = (tmpsum - 1) / (ii + 1);
+                if (tmax >= s[ii + 1]) { bget = true; break; }
+            }
+            if (!bget) tmax = (tmpsum + s[L - 1] - 1) / L;
+            for (int l = 0; l < L; ++l) ctl->alpha[l] = fmax(y[l] - tmax, 0.0);
+        }
+    }
+    const int slot = (it - 1) % TRACE_CAP;
+    F.trace[3 * slot + 0] = energy;
+    F.trace[3 * slot + 1] = ptdmu;
+    F.trace[3 * slot + 2] = ptdsig;
+    if (F.t_decay_every > 0 && it % F.t_decay_every == 0) ctl->T = fmax(ctl->T * F.drate, F.t_min);
+    ctl->it = it + 1;
+    ctl->done = ctl->done + 1;
+    if (ptdmu < F.tor) ctl->stop = 1;
+}
+
+template <typename R>
+__global__ void k_init_state(R *st0, R *st1, int64_t MNL, uint64_t b1, uint64_t b2, uint64_t b3,
+                             uint64_t b4, double minu, double maxu, double minv, double maxv)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= MNL) return;
+    // gqmap_gpu_mixture.m:19-24
+    const R v[NPLANES] = {R(minu + u01(b1, i) * (maxu - minu)), R(minv + u01(b2, i) * (maxv - minv)),
+                          R(u01(b3, i) + (maxu - minu)),        R(u01(b4, i) + (maxv - minv)),
+                          R(0), R(0), R(0), R(0), R(0)};
+#pragma unroll
+    for (int q = 0; q < NPLANES; ++q) {
+        st0[i + MNL * q] = v[q];
+        st1[i + MNL * q] = v[q];
+    }
+}
+
+// profile_logP (gqmap_gpu_mixture.m:148-154; super :152-169): per-block partials.
+template <typename R, bool SUPER>
+__global__ __launch_bounds__(256) void k_logp(IterParams<R> P, const R *__restrict__ map,
+                                              double *partials)
+{
+    const int64_t MN = (int64_t)P.M * P.N;
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    double v = 0;
+    if (i < MN) {
+        const int m = (int)(i % P.M), n = (int)(i / P.M);
+        if (m >= 1 && m <= P.M - 2 && n >= 1 && n <= P.N - 2) {
+            const R u = map[i], w = map[i + MN];
+            if constexpr (!SUPER) {
+                const R d = P.I1[m + (int64_t)P.Mo * n] - sample(P.VV, P.M2, P.Mo, P.No, m + 1, n + 1, u, w);
+                v += (double)(-P.lamd * dsqrt(P.epsn + d * d));
+            } else {
+                for (int q = 0; q < 16; ++q) {
+                    const int ii = 4 * m + (q & 3), jj = 4 * n + (q >> 2);
+                    const R d = P.I1[ii + (int64_t)P.Mo * jj] -
+                                sample(P.VV, P.M2, P.Mo, P.No, ii + 1, jj + 1, u, w);
+                    v += (double)(-P.lamd * dsqrt(P.epsn + d * d));
+                }
+            }
+            // edge_pot(cat(4,uv,uv), cat(4,circshift(uv,-1),circshift(uv,-1,2)))
+            const int64_t jd = (m + 1) % P.M + (int64_t)P.M * n;
+            const int64_t jr = m + (int64_t)P.M * ((n + 1) % P.N);
+            for (int c = 0; c < 2; ++c) {
+                const R x = map[i + MN * c];
+                const R dd = x - map[jd + MN * c], dr = x - map[jr + MN * c];
+                v += (double)(-P.lams * dsqrt(P.epsn + dd * dd));
+                v += (double)(-P.lams * dsqrt(P.epsn + dr * dr));
+            }
+        }
+    }
+    __shared__ double red[4];
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+}  // namespace gq
+
+// ===========================================================================
+// host runtime
+// ===========================================================================
+using namespace gq;
+
+namespace gq {
+hipError_t mixture_map_device(const double *alpha_host, const void *st, bool fp32, int64_t MNL,
+                              int M, int N, int L, double *out_dev, hipStream_t s);
+}
+
+struct gqmap_ctx {
+    gqmap_options opt;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool fp32 = false, super_ = false;
+    int Mo = 0, No = 0, M = 0, N = 0, L = 0, K = 0, K2 = 0;
+    int64_t MNL = 0;
+    size_t rsz = 8;
+    void *d_VV = nullptr, *d_I1 = nullptr, *d_st[2] = {nullptr, nullptr}, *d_tab = nullptr;
+    Ctl *d_ctl = nullptr;
+    double *d_partials = nullptr, *d_trace = nullptr;
+    int tiles_m = 0, tiles_n = 0, nblocks = 0;
+    bool have_images = false, have_state = false;
+    hipGraphExec_t graph = nullptr;
+    double tab_host[NTAB * TS];
+};
+
+namespace {
+
+gqmap_status alloc_grid(gqmap_ctx *c)
+{
+    c->tiles_m = (c->M + TILE - 1) / TILE;
+    c->tiles_n = (c->N + TILE - 1) / TILE;
+    c->nblocks = c->tiles_m * c->tiles_n;
+    const size_t bytes = (size_t)c->MNL * NPLANES * c->rsz;
+    for (int b = 0; b < 2; ++b) {
+        if (c->d_st[b]) (void)hipFree(c->d_st[b]);
+        c->d_st[b] = nullptr;
+        GQ_HIP(hipMalloc(&c->d_st[b], bytes));
+    }
+    if (c->d_partials) (void)hipFree(c->d_partials);
+    c->d_partials = nullptr;
+    GQ_HIP(hipMalloc(&c->d_partials, sizeof(double) * (size_t)c->nblocks * (3 + c->L) + 64));
+    return GQMAP_OK;
+}
+
+template <typename R>
+IterParams<R> iter_params(const gqmap_ctx *c)
+{
+    IterParams<R> P;
+    const gqmap_options &o = c->opt;
+    P.VV = (const R *)c->d_VV;
+    P.I1 = (const R *)c->d_I1;
+    P.st0 = (R *)c->d_st[0];
+    P.st1 = (R *)c->d_st[1];
+    P.tab = (const R *)c->d_tab;
+    P.ctl = c->d_ctl;
+    P.partials = c->d_partials;
+    P.M = c->M; P.N = c->N; P.Mo = c->Mo; P.No = c->No; P.M2 = c->Mo + 2;
+    P.L = c->L; P.K2 = c->K2;
+    P.tiles_m = c->tiles_m; P.tiles_n = c->tiles_n;
+    P.epsn = R(o.epsn); P.lamd = R(o.lambdad); P.lams = R(o.lambdas);
+    P.minu = R(o.minu); P.maxu = R(o.maxu); P.minv = R(o.minv); P.maxv = R(o.maxv);
+    P.sig_lo = R(o.sig_lo); P.sig_hi = R(o.sig_hi); P.corr = R(o.corr_tor);
+    P.step0 = o.step0; P.step_decay = o.step_decay;
+    P.guard = o.guard_a;
+    P.MNL = c->MNL;
+    return P;
+}
+
+FinParams fin_params(const gqmap_ctx *c)
+{
+    FinParams F;
+    const gqmap_options &o = c->opt;
+    F.partials = c->d_partials;
+    F.nblocks = c->nblocks;
+    F.L = c->L;
+    F.ctl = c->d_ctl;
+    F.trace = c->d_trace;
+    F.count = (double)(c->M - 2) * (double)(c->N - 2) * c->L;
+    F.step0 = o.step0; F.step_decay = o.step_decay;
+    F.alpha_mode = o.alpha_mode; F.alpha_start = o.alpha_start; F.alpha_lr = o.alpha_lr;
+    F.t_decay_every = o.t_decay_every; F.drate = o.drate; F.t_min = o.t_min; F.tor = o.tor;
+    return F;
+}
+
+template <typename R, bool SUPER>
+void launch_iter_t(gqmap_ctx *c)
+{
+    k_iter<R, SUPER><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R>(c));
+}
+
+void launch_iter(gqmap_ctx *c)
+{
+    if (c->fp32) {
+        if (c->super_) launch_iter_t<float, true>(c);
+        else launch_iter_t<float, false>(c);
+    } else {
+        if (c->super_) launch_iter_t<double, true>(c);
+        else launch_iter_t<double, false>(c);
+    }
+}
+
+void launch_finalize(gqmap_ctx *c) { k_finalize<<<1, 256, 0, c->stream>>>(fin_params(c)); }
+
+gqmap_status upload_ctl(gqmap_ctx *c, int it, double T, const double *w, const double *alpha)
+{
+    Ctl h{};
+    h.it = it;
+    h.done = 0;
+    h.stop = 0;
+    h.T = T;
+    for (int l = 0; l < c->L; ++l) {
+        h.w[l] = w[l];
+        h.alpha[l] = alpha[l];
+    }
+    GQ_HIP(hipMemcpyAsync(c->d_ctl, &h, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    return GQMAP_OK;
+}
+
+gqmap_status read_ctl(gqmap_ctx *c, Ctl *h)
+{
+    GQ_HIP(hipMemcpyAsync(h, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    return GQMAP_OK;
+}
+
+gqmap_status ensure_graph(gqmap_ctx *c)
+{
+    if (c->graph) return GQMAP_OK;
+    hipGraph_t g;
+    GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < GRAPH_CHUNK; ++i) {
+        launch_iter(c);
+        launch_finalize(c);
+    }
+    GQ_HIP(hipStreamEndCapture(c->stream, &g));
+    hipError_t e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    GQ_HIP(e);
+    return GQMAP_OK;
+}
+
+void drop_graph(gqmap_ctx *c)
+{
+    if (c->graph) (void)hipGraphExecDestroy(c->graph);
+    c->graph = nullptr;
+}
+
+template <typename R>
+std::vector<R> convert(const double *p, size_t n)
+{
+    std::vector<R> v(n);
+    for (size_t i = 0; i < n; ++i) v[i] = R(p[i]);
+    return v;
+}
+
+gqmap_status upload(gqmap_ctx *c, void *dst, const double *src, size_t n)
+{
+    if (c->fp32) {
+        std::vector<float> v = convert<float>(src, n);
+        GQ_HIP(hipMemcpyAsync(dst, v.data(), n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+    } else {
+        GQ_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+    }
+    return GQMAP_OK;
+}
+
+gqmap_status download(gqmap_ctx *c, double *dst, const void *src, size_t n)
+{
+    if (c->fp32) {
+        std::vector<float> v(n);
+        GQ_HIP(hipMemcpyAsync(v.data(), src, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+        for (size_t i = 0; i < n; ++i) dst[i] = v[i];
+    } else {
+        GQ_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+    }
+    return GQMAP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gqmap_abi_version(void) { return GQMAP_ABI_VERSION; }
+
+void gqmap_options_default(gqmap_options *o, int engine)
+{
+    std::memset(o, 0, sizeof(*o));
+    const bool sup = engine == GQMAP_ENGINE_SUPER;
+    // driver values: optical_flow.m:16-23 / optical_flowSuper.m:19-26
+    o->its = 30000;
+    o->K = sup ? 11 : 9;
+    o->L = 3;
+    o->temperature = sup ? 0.2 : 0.0;
+    o->drate = sup ? 0.75 : 0.5;
+    o->epsn = 1e-6;
+    o->lambdad = 1.0;
+    o->lambdas = sup ? 16.0 : 5.0;
+    o->minu = -1; o->maxu = 1; o->minv = -1; o->maxv = 1;
+    o->engine = engine;
+    o->precision = GQMAP_FP64;
+    o->alpha_mode = GQMAP_ALPHA_SOFTMAX;
+    o->alpha_start = 500;
+    o->alpha_lr = 1e-7;
+    o->guard_a = sup ? 0 : 1;
+    o->t_decay_every = sup ? 500 : 0;
+    o->t_min = 0.001;
+    o->step0 = sup ? 0.001 : 0.1;
+    o->step_decay = sup ? 4000.0 : 8000.0;
+    o->sig_lo = 0.01;
+    o->sig_hi = sup ? 25.0 : 23.0;
+    o->corr_tor = 1 - 1e-5;
+    o->tor = 1e-4;
+}
+
+gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
+{
+    clear_error();
+    GQ_CHECK(out && opt, GQMAP_ERR_INVALID_ARG, "gqmap_create: null argument");
+    *out = nullptr;
+    GQ_CHECK(opt->L >= 1 && opt->L <= GQMAP_LMAX, GQMAP_ERR_INVALID_ARG, "L=%d outside [1,%d]",
+             opt->L, GQMAP_LMAX);
+    GQ_CHECK(opt->K >= 2 && opt->K <= GQMAP_KMAX, GQMAP_ERR_INVALID_ARG, "K=%d outside [2,%d]",
+             opt->K, GQMAP_KMAX);
+    GQ_CHECK(opt->engine == GQMAP_ENGINE_MIXTURE || opt->engine == GQMAP_ENGINE_SUPER,
+             GQMAP_ERR_INVALID_ARG, "unknown engine %d", opt->engine);
+    GQ_CHECK(opt->precision == GQMAP_FP64 || opt->precision == GQMAP_FP32, GQMAP_ERR_INVALID_ARG,
+             "unknown precision %d", opt->precision);
+    GQ_CHECK(opt->minu <= opt->maxu && opt->minv <= opt->maxv, GQMAP_ERR_INVALID_ARG,
+             "empty flow range");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_error("no HIP device available");
+        return GQMAP_ERR_NO_DEVICE;
+    }
+    GQ_CHECK(device >= 0 && device < ndev, GQMAP_ERR_INVALID_ARG, "device %d of %d", device, ndev);
+    DeviceGuard dg(device);
+    gqmap_ctx *c = new gqmap_ctx();
+    c->opt = *opt;
+    c->device = device;
+    c->fp32 = opt->precision == GQMAP_FP32;
+    c->super_ = opt->engine == GQMAP_ENGINE_SUPER;
+    c->rsz = c->fp32 ? sizeof(float) : sizeof(double);
+    c->L = opt->L;
+    c->K = opt->K;
+    c->K2 = opt->K * opt->K;
+    // quadrature tables, MATLAB meshgrid order k = r + K*c (gqmap_gpu_mixture.m:8-10)
+    double X[GQMAP_KMAX], W[GQMAP_KMAX];
+    if (gauss_hermite(c->K, X, W) != 0) {
+        delete c;
+        set_error("Gauss-Hermite did not converge for K=%d", opt->K);
+        return GQMAP_ERR_INVALID_ARG;
+    }
+    std::memset(c->tab_host, 0, sizeof(c->tab_host));
+    for (int cc = 0; cc < c->K; ++cc)
+        for (int r = 0; r < c->K; ++r) {
+            const int k = r + c->K * cc;
+            const double xi = X[cc], xj = X[r], w = W[cc] * W[r];
+            c->tab_host[0 * TS + k] = xi;
+            c->tab_host[1 * TS + k] = xj;
+            c->tab_host[2 * TS + k] = w;
+            c->tab_host[3 * TS + k] = w * xi;
+            c->tab_host[4 * TS + k] = w * xj;
+            c->tab_host[5 * TS + k] = w * (xi * xi + xj * xj);
+            c->tab_host[6 * TS + k] = w * (xi * xi - xj * xj);
+            c->tab_host[7 * TS + k] = w * (xi * xj);
+        }
+    gqmap_status st = GQMAP_OK;
+    auto fail = [&](gqmap_status s) { gqmap_destroy(c); return s; };
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("hipStreamCreate failed");
+        return fail(GQMAP_ERR_HIP);
+    }
+    if (hipMalloc(&c->d_tab, NTAB * TS * c->rsz) != hipSuccess ||
+        hipMalloc((void **)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
+        hipMalloc((void **)&c->d_trace, sizeof(double) * 3 * TRACE_CAP) != hipSuccess) {
+        set_error("device allocation failed");
+        return fail(GQMAP_ERR_OUT_OF_MEMORY);
+    }
+    if ((st = upload(c, c->d_tab, c->tab_host, NTAB * TS)) != GQMAP_OK) return fail(st);
+    *out = c;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, int Mo, int No)
+{
+    clear_error();
+    GQ_CHECK(c && I1 && I2, GQMAP_ERR_INVALID_ARG, "gqmap_set_images: null argument");
+    GQ_CHECK(Mo >= 4 && No >= 4, GQMAP_ERR_INVALID_ARG, "image %dx%d too small", Mo, No);
+    if (c->super_)
+        GQ_CHECK(Mo % 4 == 0 && No % 4 == 0, GQMAP_ERR_INVALID_ARG,
+                 "super engine needs Mo,No divisible by 4 (got %dx%d)", Mo, No);
+    DeviceGuard dg(c->device);
+    const bool resize = Mo != c->Mo || No != c->No;
+    c->Mo = Mo;
+    c->No = No;
+    c->M = c->super_ ? Mo / 4 : Mo;
+    c->N = c->super_ ? No / 4 : No;
+    GQ_CHECK(c->M >= 3 && c->N >= 3, GQMAP_ERR_INVALID_ARG, "node grid %dx%d has no interior",
+             c->M, c->N);
+    c->MNL = (int64_t)c->M * c->N * c->L;
+    std::vector<double> VV((size_t)(Mo + 2) * (No + 2));
+    build_padded(I2, Mo, No, VV.data());
+    if (resize || !c->d_VV) {
+        drop_graph(c);
+        if (c->d_VV) (void)hipFree(c->d_VV);
+        if (c->d_I1) (void)hipFree(c->d_I1);
+        c->d_VV = c->d_I1 = nullptr;
+        GQ_HIP(hipMalloc(&c->d_VV, VV.size() * c->rsz));
+        GQ_HIP(hipMalloc(&c->d_I1, (size_t)Mo * No * c->rsz));
+        gqmap_status s = alloc_grid(c);
+        if (s != GQMAP_OK) return s;
+        c->have_state = false;
+    }
+    gqmap_status s;
+    if ((s = upload(c, c->d_VV, VV.data(), VV.size())) != GQMAP_OK) return s;
+    if ((s = upload(c, c->d_I1, I1, (size_t)Mo * No)) != GQMAP_OK) return s;
+    c->have_images = true;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_init_state(gqmap_ctx *c, uint64_t seed)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "gqmap_init_state before gqmap_set_images");
+    DeviceGuard dg(c->device);
+    const gqmap_options &o = c->opt;
+    const int threads = 256;
+    const int blocks = (int)((c->MNL + threads - 1) / threads);
+    const uint64_t b1 = stream_base(seed, 1), b2 = stream_base(seed, 2);
+    const uint64_t b3 = stream_base(seed, 3), b4 = stream_base(seed, 4);
+    if (c->fp32)
+        k_init_state<float><<<blocks, threads, 0, c->stream>>>(
+            (float *)c->d_st[0], (float *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv);
+    else
+        k_init_state<double><<<blocks, threads, 0, c->stream>>>(
+            (double *)c->d_st[0], (double *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv);
+    GQ_HIP(hipGetLastError());
+    double w[GQMAP_LMAX], alpha[GQMAP_LMAX], se = 0;
+    gqmap_rand_uniform(seed, 0, 0, (size_t)c->L, w);  // w = rand(1,1,L)
+    for (int l = 0; l < c->L; ++l) se += std::exp(w[l]);
+    for (int l = 0; l < c->L; ++l) alpha[l] = std::exp(w[l]) / se;
+    gqmap_status s = upload_ctl(c, 1, o.temperature, w, alpha);
+    if (s != GQMAP_OK) return s;
+    c->have_state = true;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_set_state(gqmap_ctx *c, const gqmap_state *st)
+{
+    clear_error();
+    GQ_CHECK(c && st, GQMAP_ERR_INVALID_ARG, "gqmap_set_state: null argument");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "gqmap_set_state before gqmap_set_images");
+    GQ_CHECK(st->muu && st->muv && st->sigu && st->sigv && st->pn && st->rou && st->w && st->alpha,
+             GQMAP_ERR_INVALID_ARG, "gqmap_set_state: null state array");
+    GQ_CHECK(st->it >= 1, GQMAP_ERR_INVALID_ARG, "state.it must be >= 1");
+    DeviceGuard dg(c->device);
+    const double *planes[NPLANES] = {st->muu, st->muv, st->sigu, st->sigv, st->pn,
+                                     st->rou, st->rou + c->MNL, st->rou + 2 * c->MNL,
+                                     st->rou + 3 * c->MNL};
+    for (int b = 0; b < 2; ++b)
+        for (int q = 0; q < NPLANES; ++q) {
+            gqmap_status s = upload(c, (char *)c->d_st[b] + (size_t)q * c->MNL * c->rsz, planes[q],
+                                    (size_t)c->MNL);
+            if (s != GQMAP_OK) return s;
+        }
+    gqmap_status s = upload_ctl(c, st->it, st->T, st->w, st->alpha);
+    if (s != GQMAP_OK) return s;
+    c->have_state = true;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_get_state(gqmap_ctx *c, gqmap_state *st)
+{
+    clear_error();
+    GQ_CHECK(c && st, GQMAP_ERR_INVALID_ARG, "gqmap_get_state: null argument");
+    GQ_CHECK(c->have_state, GQMAP_ERR_STATE, "no state");
+    DeviceGuard dg(c->device);
+    Ctl h;
+    gqmap_status s = read_ctl(c, &h);
+    if (s != GQMAP_OK) return s;
+    const void *cur = c->d_st[h.done & 1];
+    double *planes[NPLANES] = {st->muu, st->muv, st->sigu, st->sigv, st->pn, st->rou,
+                               st->rou ? st->rou + c->MNL : nullptr,
+                               st->rou ? st->rou + 2 * c->MNL : nullptr,
+                               st->rou ? st->rou + 3 * c->MNL : nullptr};
+    for (int q = 0; q < NPLANES; ++q) {
+        if (!planes[q]) continue;
+        s = download(c, planes[q], (const char *)cur + (size_t)q * c->MNL * c->rsz, (size_t)c->MNL);
+        if (s != GQMAP_OK) return s;
+    }
+    for (int l = 0; l < c->L; ++l) {
+        if (st->w) st->w[l] = h.w[l];
+        if (st->alpha) st->alpha[l] = h.alpha[l];
+    }
+    st->it = h.it;
+    st->T = h.T;
+    return GQMAP_OK;
+}
+
+static gqmap_status fetch_trace(gqmap_ctx *c, int it_before, int n, double *trace)
+{
+    if (!trace || n <= 0) return GQMAP_OK;
+    std::vector<double> ring((size_t)3 * TRACE_CAP);
+    GQ_HIP(hipMemcpyAsync(ring.data(), c->d_trace, ring.size() * sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) {
+        const int slot = (it_before + i - 1) % TRACE_CAP;
+        for (int q = 0; q < 3; ++q) trace[3 * i + q] = ring[3 * slot + q];
+    }
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_run(gqmap_ctx *c, int n_iter, int *n_done, double *trace)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    GQ_CHECK(c->have_images && c->have_state, GQMAP_ERR_STATE, "gqmap_run before images/state");
+    GQ_CHECK(n_iter >= 0, GQMAP_ERR_INVALID_ARG, "n_iter < 0");
+    DeviceGuard dg(c->device);
+    Ctl h0;
+    gqmap_status s = read_ctl(c, &h0);
+    if (s != GQMAP_OK) return s;
+    int total = 0;
+    while (total < n_iter) {
+        // the device trace ring holds TRACE_CAP iterations: drain it per chunk
+        const int chunk = std::min(n_iter - total, TRACE_CAP);
+        int left = chunk;
+        if (left >= GRAPH_CHUNK) {
+            if ((s = ensure_graph(c)) != GQMAP_OK) return s;
+            while (left >= GRAPH_CHUNK) {
+                GQ_HIP(hipGraphLaunch(c->graph, c->stream));
+                left -= GRAPH_CHUNK;
+            }
+        }
+        for (; left > 0; --left) {
+            launch_iter(c);
+            launch_finalize(c);
+        }
+        GQ_HIP(hipGetLastError());
+        Ctl h;
+        if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+        const int ran = h.it - (h0.it + total);
+        if ((s = fetch_trace(c, h0.it + total, ran, trace ? trace + 3 * total : nullptr)) != GQMAP_OK)
+            return s;
+        total += ran;
+        if (h.stop || ran < chunk) break;
+    }
+    if (n_done) *n_done = total;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *total_ms,
+                             double *iter_kernel_ms)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    GQ_CHECK(c->have_images && c->have_state, GQMAP_ERR_STATE, "gqmap_run before images/state");
+    GQ_CHECK(n_iter >= 1, GQMAP_ERR_INVALID_ARG, "n_iter < 1");
+    DeviceGuard dg(c->device);
+    Ctl h0;
+    gqmap_status s = read_ctl(c, &h0);
+    if (s != GQMAP_OK) return s;
+    std::vector<hipEvent_t> ev((size_t)2 * n_iter + 2);
+    for (auto &e : ev) GQ_HIP(hipEventCreate(&e));
+    GQ_HIP(hipEventRecord(ev[0], c->stream));
+    for (int i = 0; i < n_iter; ++i) {
+        GQ_HIP(hipEventRecord(ev[2 + 2 * i], c->stream));
+        launch_iter(c);
+        GQ_HIP(hipEventRecord(ev[3 + 2 * i], c->stream));
+        launch_finalize(c);
+    }
+    GQ_HIP(hipEventRecord(ev[1], c->stream));
+    GQ_HIP(hipEventSynchronize(ev[1]));
+    GQ_HIP(hipGetLastError());
+    float t = 0;
+    GQ_HIP(hipEventElapsedTime(&t, ev[0], ev[1]));
+    double sum = 0;
+    for (int i = 0; i < n_iter; ++i) {
+        float k = 0;
+        GQ_HIP(hipEventElapsedTime(&k, ev[2 + 2 * i], ev[3 + 2 * i]));
+        sum += k;
+    }
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    Ctl h;
+    if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+    if (n_done) *n_done = h.it - h0.it;
+    if (total_ms) *total_ms = t;
+    if (iter_kernel_ms) *iter_kernel_ms = sum;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_get_info(gqmap_ctx *c, gqmap_info *info)
+{
+    clear_error();
+    GQ_CHECK(c && info, GQMAP_ERR_INVALID_ARG, "null argument");
+    DeviceGuard dg(c->device);
+    std::memset(info, 0, sizeof(*info));
+    info->Mo = c->Mo; info->No = c->No; info->M = c->M; info->N = c->N;
+    info->L = c->L; info->K = c->K; info->device = c->device;
+    if (c->have_state) {
+        Ctl h;
+        gqmap_status s = read_ctl(c, &h);
+        if (s != GQMAP_OK) return s;
+        info->it = h.it;
+        info->stopped = h.stop;
+        info->T = h.T;
+    }
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_get_map(gqmap_ctx *c, double *map)
+{
+    clear_error();
+    GQ_CHECK(c && map, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->have_state, GQMAP_ERR_STATE, "no state");
+    DeviceGuard dg(c->device);
+    Ctl h;
+    gqmap_status s = read_ctl(c, &h);
+    if (s != GQMAP_OK) return s;
+    const void *cur = c->d_st[h.done & 1];
+    const size_t MN = (size_t)c->M * c->N;
+    if (c->L == 1) {  // map = cat(3, mu_u, mu_v)  (gqmap_gpu_mixture.m:55)
+        if ((s = download(c, map, cur, MN)) != GQMAP_OK) return s;
+        return download(c, map + MN, (const char *)cur + (size_t)c->MNL * c->rsz, MN);
+    }
+    double *d_out = nullptr;
+    GQ_HIP(hipMalloc(&d_out, sizeof(double) * 2 * MN));
+    hipError_t e = mixture_map_device(h.alpha, cur, c->fp32, c->MNL, c->M, c->N, c->L, d_out, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(map, d_out, sizeof(double) * 2 * MN, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_out);
+    GQ_HIP(e);
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_log_p(gqmap_ctx *c, const double *map, double *logp)
+{
+    clear_error();
+    GQ_CHECK(c && map && logp, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "no images");
+    DeviceGuard dg(c->device);
+    const size_t MN = (size_t)c->M * c->N;
+    const int blocks = (int)((MN + 255) / 256);
+    void *d_map = nullptr;
+    double *d_part = nullptr;
+    GQ_HIP(hipMalloc(&d_map, 2 * MN * c->rsz));
+    GQ_HIP(hipMalloc(&d_part, sizeof(double) * blocks));
+    gqmap_status s = upload(c, d_map, map, 2 * MN);
+    if (s == GQMAP_OK) {
+        if (c->fp32) {
+            if (c->super_) k_logp<float, true><<<blocks, 256, 0, c->stream>>>(iter_params<float>(c), (const float *)d_map, d_part);
+            else k_logp<float, false><<<blocks, 256, 0, c->stream>>>(iter_params<float>(c), (const float *)d_map, d_part);
+        } else {
+            if (c->super_) k_logp<double, true><<<blocks, 256, 0, c->stream>>>(iter_params<double>(c), (const double *)d_map, d_part);
+            else k_logp<double, false><<<blocks, 256, 0, c->stream>>>(iter_params<double>(c), (const double *)d_map, d_part);
+        }
+        std::vector<double> part(blocks);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(part.data(), d_part, sizeof(double) * blocks, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            set_error("gqmap_log_p: %s", hipGetErrorString(e));
+            s = GQMAP_ERR_HIP;
+        }
+        double v = 0;
+        for (double x : part) v += x;
+        *logp = v;
+    }
+    (void)hipFree(d_map);
+    (void)hipFree(d_part);
+    return s;
+}
+
+gqmap_status gqmap_synchronize(gqmap_ctx *c)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    DeviceGuard dg(c->device);
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    return GQMAP_OK;
+}
+
+void gqmap_destroy(gqmap_ctx *c)
+{
+    if (!c) return;
+    DeviceGuard dg(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    drop_graph(c);
+    void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, c->d_partials, c->d_trace};
+    for (void *p : bufs)
+        if (p) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+}  // extern "C"

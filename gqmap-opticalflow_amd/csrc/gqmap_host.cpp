@@ -1,0 +1,122 @@
+// gqmap_host.cpp -- host-side helpers of libgqmap.so (no device code).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "gqmap_internal.h"
+
+namespace gq {
+
+static thread_local std::string g_err;
+
+void set_error(const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+void clear_error() { g_err.clear(); }
+
+// getVV (gqmap_gpu_mixture.m:191-208): copy I2 into the interior of an
+// (M+2)x(N+2) array, then extrapolate the first/last row of every column and
+// afterwards the first/last column of every row with 3*f1 - 3*f2 + f3 -- the
+// boundary rule of MATLAB interp2(...,'cubic').  Column-major throughout.
+void build_padded(const double *I2, int M, int N, double *VV)
+{
+    const int M2 = M + 2, N2 = N + 2;
+    std::fill(VV, VV + (size_t)M2 * N2, 0.0);
+    for (int n = 0; n < N; ++n)
+        std::memcpy(VV + (size_t)M2 * (n + 1) + 1, I2 + (size_t)M * n, sizeof(double) * M);
+    for (int col = 0; col < N2; ++col) {
+        double *c = VV + (size_t)M2 * col;
+        c[0] = (3.0 * c[1] - 3.0 * c[2]) + c[3];
+        c[M2 - 1] = (3.0 * c[M2 - 2] - 3.0 * c[M2 - 3]) + c[M2 - 4];
+    }
+    double *first = VV, *last = VV + (size_t)M2 * (N2 - 1);
+    for (int r = 0; r < M2; ++r) {
+        first[r] = (3.0 * first[r + M2] - 3.0 * first[r + 2 * M2]) + first[r + 3 * M2];
+        last[r] = (3.0 * last[r - M2] - 3.0 * last[r - 2 * M2]) + last[r - 3 * M2];
+    }
+}
+
+// Gauss-Hermite nodes/weights for int exp(-x^2) f(x): Newton iteration on the
+// orthonormal Hermite recurrence with asymptotic starting guesses.  The
+// reference (GaussHermite_2.m) takes the eigen-decomposition of the Jacobi
+// matrix instead; both give the same rule (tests compare with numpy.hermgauss).
+int gauss_hermite(int n, double *x, double *w)
+{
+    if (n < 1 || n > GQMAP_KMAX) return 1;
+    const double pim4 = 0.7511255444649425;  // pi^(-1/4)
+    const int half = (n + 1) / 2;
+    double z = 0, pp = 1;
+    double xd[GQMAP_KMAX], wd[GQMAP_KMAX];  // descending
+    for (int i = 0; i < half; ++i) {
+        if (i == 0) z = std::sqrt(2.0 * n + 1) - 1.85575 * std::pow(2.0 * n + 1, -1.0 / 6.0);
+        else if (i == 1) z -= 1.14 * std::pow((double)n, 0.426) / z;
+        else if (i == 2) z = 1.86 * z - 0.86 * xd[0];
+        else if (i == 3) z = 1.91 * z - 0.91 * xd[1];
+        else z = 2.0 * z - xd[i - 2];
+        int iter = 0;
+        for (; iter < 200; ++iter) {
+            double p1 = pim4, p2 = 0.0;
+            for (int j = 1; j <= n; ++j) {
+                const double p3 = p2;
+                p2 = p1;
+                p1 = z * std::sqrt(2.0 / j) * p2 - std::sqrt((j - 1.0) / j) * p3;
+            }
+            pp = std::sqrt(2.0 * n) * p2;
+            const double z1 = z;
+            z = z1 - p1 / pp;
+            if (std::fabs(z - z1) <= 1e-15 * std::max(1.0, std::fabs(z))) break;
+        }
+        if (iter == 200) return 2;
+        xd[i] = z;
+        xd[n - 1 - i] = -z;
+        wd[i] = wd[n - 1 - i] = 2.0 / (pp * pp);
+    }
+    if (n % 2 == 1) xd[half - 1] = 0.0;  // exact symmetric middle node
+    for (int i = 0; i < n; ++i) {
+        x[i] = xd[n - 1 - i];
+        w[i] = wd[n - 1 - i];
+    }
+    return 0;
+}
+
+}  // namespace gq
+
+extern "C" {
+
+const char *gqmap_last_error(void) { return gq::g_err.c_str(); }
+
+gqmap_status gqmap_gauss_hermite(int K, double *x, double *w)
+{
+    gq::clear_error();
+    GQ_CHECK(x && w, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(K >= 1 && K <= GQMAP_KMAX, GQMAP_ERR_INVALID_ARG, "K=%d outside [1,%d]", K, GQMAP_KMAX);
+    GQ_CHECK(gq::gauss_hermite(K, x, w) == 0, GQMAP_ERR_INVALID_ARG, "Gauss-Hermite did not converge");
+    return GQMAP_OK;
+}
+
+void gqmap_rand_uniform(uint64_t seed, uint32_t stream, uint64_t first, size_t n, double *out)
+{
+    const uint64_t base = gq::stream_base(seed, stream);
+    for (size_t i = 0; i < n; ++i) out[i] = gq::u01(base, first + i);
+}
+
+int gqmap_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,165 @@
+/*
+ * gqmap.h -- C ABI of the MI355X-native QGMAP optical-flow hot path.
+ *
+ * This is the drop-in boundary.  The reference's engines are MATLAB
+ * functions called from the driver scripts:
+ *
+ *   [mu,sigma,alpha,AEPE,Energy,logP] = gqmap_gpu_mixture(options,I1,I2)
+ *        -- gqmap_gpu_mixture.m:1          (called from optical_flow.m:27)
+ *   [mu,sigma,alpha,AEPE,Energy,logP] = gqmap_gpuSuper_mix_entropy(options,I1,I2)
+ *        -- gqmap_gpuSuper_mix_entropy.m:1 (called from optical_flowSuper.m:34)
+ *   [mu,sigma,rou,AEPE,Energy]        = gqmap_ctf(options,I1,I2,GRDT)
+ *        -- legacy/gqmap_ctf.m:1           (called from legacy/optical_flow_ctf.m:33)
+ *
+ * A MEX gateway (mex/gqmap_gpu_mixture_mex.cpp) shadows
+ * the .m files on the MATLAB path and forwards to these entry points.  The
+ * host-side bookkeeping that stays in MATLAB (AEPE every 300 its, PNG
+ * snapshots, fprintf) is reproduced by the Python mirror in
+ * gqmap_opticalflow_amd/engine.py.
+ *
+ * Conventions: plain C types only; every array is caller-owned host memory in
+ * MATLAB column-major order (row index m fastest); every call returns a
+ * gqmap_status and gqmap_last_error() gives a message for the calling thread.
+ * One context per host thread; a context owns one HIP stream on one device.
+ */
+#ifndef GQMAP_H
+#define GQMAP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GQMAP_ABI_VERSION 1
+#define GQMAP_LMAX 8   /* mixture components supported (reference uses L<=3) */
+#define GQMAP_KMAX 16  /* quadrature order supported (reference uses K=9, 11) */
+
+typedef enum gqmap_status {
+    GQMAP_OK = 0,
+    GQMAP_ERR_INVALID_ARG = 1,
+    GQMAP_ERR_HIP = 2,
+    GQMAP_ERR_OUT_OF_MEMORY = 3,
+    GQMAP_ERR_NO_DEVICE = 4,
+    GQMAP_ERR_STATE = 5,       /* e.g. run before set_images / set_state       */
+    GQMAP_ERR_UNSUPPORTED = 6
+} gqmap_status;
+
+typedef enum gqmap_engine_kind {
+    GQMAP_ENGINE_MIXTURE = 0,  /* gqmap_gpu_mixture.m: one node per pixel          */
+    GQMAP_ENGINE_SUPER = 1     /* gqmap_gpuSuper_mix_entropy.m: one node per 4x4   */
+} gqmap_engine_kind;
+
+typedef enum gqmap_precision { GQMAP_FP64 = 0, GQMAP_FP32 = 1 } gqmap_precision;
+typedef enum gqmap_alpha_mode {
+    GQMAP_ALPHA_SOFTMAX = 0,   /* updateAlpha, gqmap_gpu_mixture.m:78-86 (live path)   */
+    GQMAP_ALPHA_PROJSPLX = 1   /* projsplx(alpha+dalpha*step*lr), :49 (commented out)   */
+} gqmap_alpha_mode;
+
+/* Options.  The first block mirrors the MATLAB `options` fields read by the
+ * engines (gqmap_gpu_mixture.m:3-6); the second block holds constants that
+ * are hard-coded in the reference source -- gqmap_options_default() fills
+ * them with the reference values for the chosen engine. */
+typedef struct gqmap_options {
+    int its, K, L;
+    double temperature, drate, epsn, lambdad, lambdas;
+    double minu, maxu, minv, maxv;
+    /* --- engine knobs (reference constants) --- */
+    int engine;          /* gqmap_engine_kind                                    */
+    int precision;       /* gqmap_precision                                      */
+    int alpha_mode;      /* gqmap_alpha_mode                                     */
+    int alpha_start;     /* alpha update when it > alpha_start        (500, :50) */
+    double alpha_lr;     /* 1e-7                                        (:83)     */
+    int guard_a;         /* `if a~=0` guard: 1 mixture (:98), 0 super             */
+    int t_decay_every;   /* 0 mixture (:73 commented), 500 super (super:72)       */
+    double t_min;        /* 0.001 (super:72)                                     */
+    double step0;        /* 0.1 mixture (:27), 0.001 super (super:26)            */
+    double step_decay;   /* 8000 mixture, 4000 super                             */
+    double sig_lo, sig_hi;  /* 0.01 / 23 mixture (:43-44), 0.01 / 25 super       */
+    double corr_tor;     /* 1-1e-5 (:7)                                          */
+    double tor;          /* 1e-4 stop threshold on ptdmu (:25,75)                */
+} gqmap_options;
+
+/* Engine state, MATLAB layout (M x N x L [x 2 x 2]).  M,N = node grid
+ * (image size for MIXTURE, image size / 4 for SUPER).  `it` is the index of
+ * the next iteration (1-based, as in the reference loop); T the temperature.
+ * The reference returns mu/sigma/alpha only (gqmap_gpu_mixture.m:183-185);
+ * this ABI also carries pn, rou, w so a run can be checkpointed/resumed. */
+typedef struct gqmap_state {
+    double *muu, *muv, *sigu, *sigv, *pn;  /* [M*N*L]        */
+    double *rou;                           /* [M*N*L*2*2]    */
+    double *w, *alpha;                     /* [L]            */
+    int it;
+    double T;
+} gqmap_state;
+
+typedef struct gqmap_info {
+    int Mo, No;          /* image size         */
+    int M, N, L, K;      /* node grid          */
+    int it;              /* next iteration     */
+    int stopped;         /* ptdmu < tor reached */
+    double T;
+    int device;
+} gqmap_info;
+
+typedef struct gqmap_ctx gqmap_ctx;
+
+/* ---- engine (gqmap_gpu_mixture.m / gqmap_gpuSuper_mix_entropy.m) ---- */
+void gqmap_options_default(gqmap_options *opt, int engine);
+gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device);
+/* I1,I2: Mo x No doubles (greyscale 0..255).  SUPER needs Mo,No divisible by 4.
+ * Builds the cubic-convolution padded copy of I2 (getVV, gqmap_gpu_mixture.m:191). */
+gqmap_status gqmap_set_images(gqmap_ctx *ctx, const double *I1, const double *I2, int Mo, int No);
+/* Initial state exactly as gqmap_gpu_mixture.m:18-24 with this library's
+ * counter-based RNG (SplitMix64; gqmap_rand_uniform) in place of MATLAB's
+ * rand(...,'gpuArray'), generated on the device. */
+gqmap_status gqmap_init_state(gqmap_ctx *ctx, uint64_t seed);
+gqmap_status gqmap_set_state(gqmap_ctx *ctx, const gqmap_state *st);
+gqmap_status gqmap_get_state(gqmap_ctx *ctx, gqmap_state *st);
+/* Run up to n_iter iterations (one iteration = gqmap_gpu_mixture.m:27-75
+ * minus the host evaluation block).  Stops early when ptdmu < tor.
+ * trace (optional, n_iter*3): Energy, ptdmu, ptdsigma per executed iteration. */
+gqmap_status gqmap_run(gqmap_ctx *ctx, int n_iter, int *n_done, double *trace);
+/* Same as gqmap_run with n_iter iterations, timed on the context's stream
+ * with HIP events: total_ms over all launches, iter_kernel_ms = sum of the
+ * fused iteration kernel's durations (event pair around each launch). */
+gqmap_status gqmap_run_timed(gqmap_ctx *ctx, int n_iter, int *n_done, double *total_ms,
+                             double *iter_kernel_ms);
+gqmap_status gqmap_get_info(gqmap_ctx *ctx, gqmap_info *info);
+/* Current mean |mu| flow (L==1) or mixture MAP (L>1, device get_map) as an
+ * M x N x 2 field -- the `map` of gqmap_gpu_mixture.m:53-58. */
+gqmap_status gqmap_get_map(gqmap_ctx *ctx, double *map);
+/* profile_logP (gqmap_gpu_mixture.m:148-154) of a given M x N x 2 map. */
+gqmap_status gqmap_log_p(gqmap_ctx *ctx, const double *map, double *logp);
+gqmap_status gqmap_synchronize(gqmap_ctx *ctx);
+void gqmap_destroy(gqmap_ctx *ctx);
+
+/* ---- standalone device ops (host pointers in/out) ---- */
+/* projsplx.m:15-30, applied independently to each of `ncols` columns of Y
+ * (n x ncols, column-major) -- the commented column-wise form projsplx.m:34-67. */
+gqmap_status gqmap_projsplx(const double *Y, double *X, int n, int ncols, int device);
+/* get_map_mex / findMixMax.m:39-70: mixture MAP per pixel (fminbnd, TolX 1e-4). */
+gqmap_status gqmap_mixture_map(const double *alpha, const double *muu, const double *sigu,
+                               const double *muv, const double *sigv, int M, int N, int L,
+                               double *out, int device);
+/* flowToColor_mex / legacy/flowToColor.m + computeColor.m: img M x N x 3 uint8,
+ * flo M x N x 2 (unknown zeroed), stats {minu,maxu,minv,maxv}, unknown M x N. */
+gqmap_status gqmap_flow_to_color(const double *flow, int M, int N, double max_flow,
+                                 uint8_t *img, double *flo, double *stats, uint8_t *unknown,
+                                 int device);
+
+/* ---- host helpers (no device needed) ---- */
+/* GaussHermite_2(K) (GaussHermite_2.m): nodes ascending + weights. */
+gqmap_status gqmap_gauss_hermite(int K, double *x, double *w);
+/* U(0,1) doubles of stream `stream`, indices [first, first+n): the RNG used by
+ * gqmap_init_state (stream 0 = w, 1 = muu, 2 = muv, 3 = sigmau, 4 = sigmav). */
+void gqmap_rand_uniform(uint64_t seed, uint32_t stream, uint64_t first, size_t n, double *out);
+const char *gqmap_last_error(void);
+int gqmap_abi_version(void);
+int gqmap_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GQMAP_H */

@@ -1,0 +1,302 @@
+"""Independent numpy fp64 restatement of the QGMAP iteration.
+
+TEST INFRASTRUCTURE ONLY (golden-vector generator and cross-check of the C
+oracle).  Written in the reference's own array style -- repmat/cat/circshift
+become np.broadcast/np.stack/np.roll -- rather than per-element loops, so it
+shares no code path with oracle/gqmap_oracle.c.
+
+Restates:
+  GaussHermite_2.m:21-32                 gauss_hermite (numpy.linalg.eigh)
+  gqmap_gpu_mixture.m:191-208            get_vv
+  gqmap_gpu_mixture.m:156-182            node_pot / edge_pot (vectorised)
+  gqmap_gpu_mixture.m:87-146             node/edge spectral gradients
+  gqmap_gpuSuper_mix_entropy.m:87-122    super node gradient
+  gqmap_gpu_mixture.m:26-86              one iteration (+ updateAlpha)
+  gqmap_gpuSuper_mix_entropy.m:72        temperature decay
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SQRT2 = np.sqrt(2.0)
+
+
+def gauss_hermite(K: int):
+    i = np.arange(1, K)
+    a = np.sqrt(i / 2.0)
+    CM = np.diag(a, 1) + np.diag(a, -1)
+    lam, V = np.linalg.eigh(CM)
+    ind = np.argsort(lam)
+    x = lam[ind]
+    V = V[:, ind].T
+    w = np.sqrt(np.pi) * V[:, 0] ** 2
+    return x, w
+
+
+def quad_tables(K: int):
+    X, W = gauss_hermite(K)
+    XI, XJ = np.meshgrid(X, X)          # XI(r,c)=X(c), XJ(r,c)=X(r)
+    WI, WJ = np.meshgrid(W, W)
+    # MATLAB linear order: column-major over (r,c)
+    f = lambda A: A.ravel(order="F")
+    return dict(XI=f(XI), XJ=f(XJ), WIWJ=f(WI * WJ), XIXJ=f(XI * XJ),
+                XI2aXJ2=f(XI ** 2 + XJ ** 2), XI2mXJ2=f(XI ** 2 - XJ ** 2))
+
+
+def get_vv(V: np.ndarray) -> np.ndarray:
+    M, N = V.shape
+    VV = np.zeros((M + 2, N + 2))
+    VV[1:-1, 1:-1] = V
+    VV[0, :] = (3.0 * VV[1, :] - 3.0 * VV[2, :]) + VV[3, :]
+    VV[-1, :] = (3.0 * VV[-2, :] - 3.0 * VV[-3, :]) + VV[-4, :]
+    VV[:, 0] = (3.0 * VV[:, 1] - 3.0 * VV[:, 2]) + VV[:, 3]
+    VV[:, -1] = (3.0 * VV[:, -2] - 3.0 * VV[:, -3]) + VV[:, -4]
+    return VV
+
+
+def _keys(t):
+    return (((2.0 - t) * t - 1.0) * t, (3.0 * t - 5.0) * t * t + 2.0,
+            ((4.0 - 3.0 * t) * t + 1.0) * t, (t - 1.0) * t * t)
+
+
+def interp_cubic(VV, M, N, Xq, Yq):
+    """Vectorised node_pot interpolation; Xq/Yq 1-based (any shape)."""
+    Xq = np.minimum(np.maximum(Xq, 1.0), N)
+    Yq = np.minimum(np.maximum(Yq, 1.0), M)
+    ix = np.where(Xq <= 1.0, 1, np.where(Xq <= N - 1, np.floor(Xq), N - 1)).astype(np.int64)
+    iy = np.where(Yq <= 1.0, 1, np.where(Yq <= M - 1, np.floor(Yq), M - 1)).astype(np.int64)
+    so, to = Xq - ix, Yq - iy
+    ws, wt = _keys(so), _keys(to)
+    Vq = np.zeros(np.broadcast(Xq, Yq).shape)
+    for c in range(4):
+        for r in range(4):
+            Vq = Vq + VV[iy - 1 + r, ix - 1 + c] * ws[c] * wt[r]
+    return Vq / 4
+
+
+class Engine:
+    def __init__(self, opts: dict, I1: np.ndarray, I2: np.ndarray):
+        self.o = opts
+        self.sup = opts.get("engine", "mixture") == "super"
+        self.I1 = np.asarray(I1, dtype=np.float64)
+        self.Mo, self.No = self.I1.shape
+        self.M, self.N = (self.Mo // 4, self.No // 4) if self.sup else (self.Mo, self.No)
+        self.VV = get_vv(np.asarray(I2, dtype=np.float64))
+        self.q = quad_tables(int(opts["K"]))
+        self.guard = bool(opts.get("guard_a", not self.sup))
+        self.step0 = float(opts.get("step0", 0.001 if self.sup else 0.1))
+        self.step_decay = float(opts.get("step_decay", 4000.0 if self.sup else 8000.0))
+        self.sig_hi = float(opts.get("sig_hi", 25.0 if self.sup else 23.0))
+        self.sig_lo = float(opts.get("sig_lo", 0.01))
+        self.corr = float(opts.get("corr_tor", 1 - 1e-5))
+        self.alpha_start = int(opts.get("alpha_start", 500))
+        self.alpha_lr = float(opts.get("alpha_lr", 1e-7))
+        self.t_every = int(opts.get("t_decay_every", 500 if self.sup else 0))
+        self.t_min = float(opts.get("t_min", 0.001))
+
+    # --- potentials -------------------------------------------------
+    def node_pot(self, x1, x2, ms, ns):
+        o = self.o
+        if not self.sup:
+            Vq = interp_cubic(self.VV, self.Mo, self.No, ns + x1, ms + x2)
+            I = self.I1[ms - 1, ns - 1]
+            return -o["lambdad"] * np.sqrt(o["epsn"] + (I - Vq) ** 2)
+        tot = np.zeros(np.broadcast(x1, ms).shape)
+        for di in range(4):
+            for dj in range(4):
+                i = 4 * ms - 3 + di
+                j = 4 * ns - 3 + dj
+                Vq = interp_cubic(self.VV, self.Mo, self.No, j + x1, i + x2)
+                tot = tot + (-o["lambdad"] * np.sqrt(o["epsn"] + (self.I1[i - 1, j - 1] - Vq) ** 2))
+        return tot
+
+    def edge_pot(self, x1, x2):
+        return -self.o["lambdas"] * np.sqrt(self.o["epsn"] + (x1 - x2) ** 2)
+
+    def _spectral(self, pot_fn, a, u1, u2, o1, o2, p):
+        q = self.q
+        s = (np.sqrt(1 + p) + np.sqrt(1 - p)) / 2
+        t = (np.sqrt(1 + p) - np.sqrt(1 - p)) / 2
+        pr = 1 - p ** 2
+        sqrtpr = np.sqrt(pr)
+        acc = {k: np.zeros_like(u1) for k in ("dp", "du1", "du2", "do1", "do2", "Ei")}
+        live = (a != 0) if self.guard else np.ones_like(u1, dtype=bool)
+        for k in range(q["XI"].size):
+            zi = s * q["XI"][k] + t * q["XJ"][k]
+            zj = t * q["XI"][k] + s * q["XJ"][k]
+            x1 = SQRT2 * o1 * zi + u1
+            x2 = SQRT2 * o2 * zj + u2
+            fval = q["WIWJ"][k] * pot_fn(x1, x2)
+            fl = np.where(live, fval, 0.0)
+            acc["dp"] += fl * (p - p * q["XI2aXJ2"][k] + 2 * q["XIXJ"][k])
+            acc["du1"] += fl * (zi - p * zj)
+            acc["du2"] += fl * (zj - p * zi)
+            acc["do1"] += fl * (q["XI2aXJ2"][k] - 1 + q["XI2mXJ2"][k] / sqrtpr)
+            acc["do2"] += fl * (q["XI2aXJ2"][k] - 1 - q["XI2mXJ2"][k] / sqrtpr)
+            acc["Ei"] += fval
+        return acc, pr, sqrtpr
+
+    def node_grad(self, T, a, u1, u2, o1, o2, p, ms, ns):
+        const1 = 1 + np.log(2 * np.pi)
+        acc, pr, sqrtpr = self._spectral(lambda x1, x2: self.node_pot(x1, x2, ms, ns),
+                                         a, u1, u2, o1, o2, p)
+        du1 = a * acc["du1"] * (SQRT2 / (o1 * pr)) / np.pi
+        du2 = a * acc["du2"] * (SQRT2 / (o2 * pr)) / np.pi
+        da = acc["Ei"] / np.pi - 3 * T * (const1 + np.log(sqrtpr * o1 * o2))
+        do1 = a * (acc["do1"] / np.pi - 3 * T) / o1
+        do2 = a * (acc["do2"] / np.pi - 3 * T) / o2
+        dp = a * (acc["dp"] / np.pi + 3 * T * p) / pr
+        return da, du1, du2, do1, do2, dp, a * da
+
+    def edge_grad(self, T, a, u1, u2, o1, o2, p):
+        const1 = 1 + np.log(2 * np.pi)
+        acc, pr, sqrtpr = self._spectral(self.edge_pot, a, u1, u2, o1, o2, p)
+        du1 = a * acc["du1"] * (SQRT2 / (o1 * pr)) / np.pi
+        du2 = a * acc["du2"] * (SQRT2 / (o2 * pr)) / np.pi
+        da = acc["Ei"] / np.pi + T * (const1 + np.log(sqrtpr * o1 * o2))
+        do1 = a * (acc["do1"] / np.pi + T) / o1
+        do2 = a * (acc["do2"] / np.pi + T) / o2
+        dp = a * (acc["dp"] / np.pi - T * p) / pr
+        return da, du1, du2, do1, do2, dp, a * da
+
+    # --- one iteration (gqmap_gpu_mixture.m:27-75) --------------------
+    def gradients(self, st: dict, T: float):
+        M, N, L = self.M, self.N, st["muu"].shape[2]
+        ns, ms = np.meshgrid(np.arange(1, N + 1), np.arange(1, M + 1))
+        ms3 = np.repeat(ms[:, :, None], L, axis=2)
+        ns3 = np.repeat(ns[:, :, None], L, axis=2)
+        A = np.broadcast_to(st["alpha"].reshape(1, 1, L), (M, N, L))
+        node = self.node_grad(T, A, st["muu"], st["muv"], st["sigu"], st["sigv"], st["pn"], ms3, ns3)
+        sh = lambda X: (np.roll(X, -1, axis=0), np.roll(X, -1, axis=1))
+        cat45 = lambda Xu, Xv: np.stack([np.stack(Xu, axis=3), np.stack(Xv, axis=3)], axis=4)
+        U1 = cat45((st["muu"], st["muu"]), (st["muv"], st["muv"]))
+        U2 = cat45(sh(st["muu"]), sh(st["muv"]))
+        O1 = cat45((st["sigu"], st["sigu"]), (st["sigv"], st["sigv"]))
+        O2 = cat45(sh(st["sigu"]), sh(st["sigv"]))
+        A5 = np.broadcast_to(st["alpha"].reshape(1, 1, L, 1, 1), U1.shape)
+        edge = self.edge_grad(T, A5, U1, U2, O1, O2, st["rou"])
+        return node, edge
+
+    def iterate(self, st: dict, it: int, T: float):
+        """Apply iteration `it` in place.  Returns (Energy, ptdmu, ptdsigma, T_next)."""
+        o = self.o
+        M, N, L = self.M, self.N, st["muu"].shape[2]
+        step = self.step0 / (1 + it / self.step_decay)
+        (dan, dmuu, dmuv, dsigu, dsigv, dpn, nE), (dae, dmu1, dmu2, dsg1, dsg2, drou, eE) = \
+            self.gradients(st, T)
+        I, J = slice(1, M - 1), slice(1, N - 1)
+        dalpha = dan[I, J, :].sum(axis=(0, 1)) + dae[I, J, :, :, :].sum(axis=(0, 1, 3, 4))
+        dmuu = dmuu + dmu1[:, :, :, :, 0].sum(axis=3) + np.roll(dmu2[:, :, :, 0, 0], 1, axis=0) \
+            + np.roll(dmu2[:, :, :, 1, 0], 1, axis=1)
+        dmuv = dmuv + dmu1[:, :, :, :, 1].sum(axis=3) + np.roll(dmu2[:, :, :, 0, 1], 1, axis=0) \
+            + np.roll(dmu2[:, :, :, 1, 1], 1, axis=1)
+        dsigu = dsigu + dsg1[:, :, :, :, 0].sum(axis=3) + np.roll(dsg2[:, :, :, 0, 0], 1, axis=0) \
+            + np.roll(dsg2[:, :, :, 1, 0], 1, axis=1)
+        dsigv = dsigv + dsg1[:, :, :, :, 1].sum(axis=3) + np.roll(dsg2[:, :, :, 0, 1], 1, axis=0) \
+            + np.roll(dsg2[:, :, :, 1, 1], 1, axis=1)
+        cl = lambda x, lo, hi: np.minimum(np.maximum(x, lo), hi)
+        st["muu"][I, J] = cl(st["muu"][I, J] + dmuu[I, J] * step, o["minu"], o["maxu"])
+        st["muv"][I, J] = cl(st["muv"][I, J] + dmuv[I, J] * step, o["minv"], o["maxv"])
+        st["sigu"][I, J] = cl(st["sigu"][I, J] + dsigu[I, J] * step, self.sig_lo, self.sig_hi)
+        st["sigv"][I, J] = cl(st["sigv"][I, J] + dsigv[I, J] * step, self.sig_lo, self.sig_hi)
+        st["rou"][I, J] = cl(st["rou"][I, J] + drou[I, J] * step, -self.corr, self.corr)
+        st["pn"][I, J] = cl(st["pn"][I, J] + dpn[I, J] * step, -self.corr, self.corr)
+        energy = nE[I, J].sum() + eE[I, J].sum()
+        if it > self.alpha_start and L != 1:
+            if int(o.get("alpha_mode", 0)) == 0:
+                a = st["alpha"]
+                dw = a * (dalpha - np.sum(dalpha * a))
+                st["w"][:] = cl(st["w"] + dw * step * self.alpha_lr, -300, 300)
+                e = np.exp(st["w"])
+                st["alpha"][:] = e / e.sum()
+            else:
+                st["alpha"][:] = projsplx(st["alpha"] + dalpha * step * self.alpha_lr)
+        ptdmu = np.abs(dmuu[I, J]).mean()
+        ptdsig = np.abs(dsigu[I, J]).mean()
+        if self.t_every > 0 and it % self.t_every == 0:
+            T = max(T * float(o.get("drate", 0.5)), self.t_min)
+        return energy, ptdmu, ptdsig, T
+
+
+def projsplx(y):
+    y = np.asarray(y, dtype=np.float64).ravel()
+    m = y.size
+    s = np.sort(y)[::-1]
+    tmpsum = 0.0
+    bget = False
+    tmax = 0.0
+    for ii in range(m - 1):
+        tmpsum = tmpsum + s[ii]
+        tmax = (tmpsum - 1) / (ii + 1)
+        if tmax >= s[ii + 1]:
+            bget = True
+            break
+    if not bget:
+        tmax = (tmpsum + s[m - 1] - 1) / m
+    return np.maximum(y - tmax, 0)
+
+
+# --- flowToColor / computeColor (legacy/flowToColor.m, legacy/computeColor.m) ---
+def colorwheel():
+    RY, YG, GC, CB, BM, MR = 15, 6, 4, 11, 13, 6
+    cw = np.zeros((RY + YG + GC + CB + BM + MR, 3))
+    col = 0
+    cw[0:RY, 0] = 255
+    cw[0:RY, 1] = np.floor(255 * np.arange(RY) / RY)
+    col += RY
+    cw[col:col + YG, 0] = 255 - np.floor(255 * np.arange(YG) / YG)
+    cw[col:col + YG, 1] = 255
+    col += YG
+    cw[col:col + GC, 1] = 255
+    cw[col:col + GC, 2] = np.floor(255 * np.arange(GC) / GC)
+    col += GC
+    cw[col:col + CB, 1] = 255 - np.floor(255 * np.arange(CB) / CB)
+    cw[col:col + CB, 2] = 255
+    col += CB
+    cw[col:col + BM, 2] = 255
+    cw[col:col + BM, 0] = np.floor(255 * np.arange(BM) / BM)
+    col += BM
+    cw[col:col + MR, 2] = 255 - np.floor(255 * np.arange(MR) / MR)
+    cw[col:col + MR, 0] = 255
+    return cw
+
+
+def flow_to_color(flow, max_flow=0.0):
+    u = np.array(flow[:, :, 0], dtype=np.float64)
+    v = np.array(flow[:, :, 1], dtype=np.float64)
+    unk = (np.abs(u) > 1e9) | (np.abs(v) > 1e9)
+    u[unk] = 0
+    v[unk] = 0
+    flo = np.stack([u, v], axis=2)
+    maxu = max(-999.0, np.nanmax(u)); minu = min(999.0, np.nanmin(u))
+    maxv = max(-999.0, np.nanmax(v)); minv = min(999.0, np.nanmin(v))
+    rad = np.sqrt(u ** 2 + v ** 2)
+    maxrad = max(-1.0, np.nanmax(rad))
+    if max_flow > 0:
+        maxrad = max_flow
+    eps = np.finfo(np.float64).eps
+    u = u / (maxrad + eps)
+    v = v / (maxrad + eps)
+    nan = np.isnan(u) | np.isnan(v)
+    u[nan] = 0
+    v[nan] = 0
+    cw = colorwheel()
+    ncols = cw.shape[0]
+    rad = np.sqrt(u ** 2 + v ** 2)
+    a = np.arctan2(-v, -u) / np.pi
+    fk = (a + 1) / 2 * (ncols - 1) + 1
+    k0 = np.floor(fk).astype(np.int64)
+    k1 = k0 + 1
+    k1[k1 == ncols + 1] = 1
+    f = fk - k0
+    img = np.zeros(u.shape + (3,), dtype=np.uint8)
+    for i in range(3):
+        col0 = cw[k0 - 1, i] / 255
+        col1 = cw[k1 - 1, i] / 255
+        col = (1 - f) * col0 + f * col1
+        idx = rad <= 1
+        col[idx] = 1 - rad[idx] * (1 - col[idx])
+        col[~idx] = col[~idx] * 0.75
+        img[:, :, i] = np.clip(np.floor(255 * col * (1 - nan)), 0, 255).astype(np.uint8)
+    img[unk] = 0
+    return img, flo, (minu, maxu, minv, maxv), unk

@@ -1,0 +1,204 @@
+"""ctypes front-end for the C oracle (oracle/gqmap_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package.  The oracle is
+a literal fp64 restatement of gqmap_gpu_mixture.m / gqmap_gpuSuper_mix_entropy.m
+(see gqmap_oracle.h for the parity status).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class OrcParams(C.Structure):
+    _fields_ = [
+        ("M", C.c_int), ("N", C.c_int), ("Mo", C.c_int), ("No", C.c_int),
+        ("L", C.c_int), ("K", C.c_int), ("super_", C.c_int), ("guard_a", C.c_int),
+        ("T", C.c_double), ("drate", C.c_double), ("t_min", C.c_double),
+        ("t_decay_every", C.c_int),
+        ("epsn", C.c_double), ("lambdad", C.c_double), ("lambdas", C.c_double),
+        ("minu", C.c_double), ("maxu", C.c_double), ("minv", C.c_double), ("maxv", C.c_double),
+        ("step0", C.c_double), ("step_decay", C.c_double),
+        ("sig_lo", C.c_double), ("sig_hi", C.c_double), ("corr_tor", C.c_double),
+        ("alpha_mode", C.c_int), ("alpha_start", C.c_int), ("alpha_lr", C.c_double),
+        ("tor", C.c_double),
+    ]
+
+
+class OrcState(C.Structure):
+    _fields_ = [(n, C.POINTER(C.c_double)) for n in
+                ("muu", "muv", "sigu", "sigv", "pn", "rou", "w", "alpha")]
+
+
+def build() -> str:
+    path = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "gqmap_oracle.c")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return path
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = C.CDLL(build())
+        d = C.POINTER(C.c_double)
+        _LIB.orc_run.restype = C.c_int
+        _LIB.orc_run.argtypes = [C.POINTER(OrcParams), d, d, C.POINTER(OrcState), d,
+                                 C.c_int, C.c_int, d, C.c_int]
+        _LIB.orc_interp_cubic.restype = C.c_double
+        _LIB.orc_interp_cubic.argtypes = [d, C.c_int, C.c_int, C.c_double, C.c_double]
+        _LIB.orc_aepe.restype = C.c_double
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _f64(a):
+    return np.require(a, dtype=np.float64, requirements=["F_CONTIGUOUS", "ALIGNED", "WRITEABLE"])
+
+
+def gauss_hermite(K: int):
+    x = np.zeros(K); w = np.zeros(K)
+    lib().orc_gauss_hermite(C.c_int(K), _p(x), _p(w))
+    return x, w
+
+
+def get_vv(I2: np.ndarray) -> np.ndarray:
+    I2 = _f64(I2)
+    M, N = I2.shape
+    VV = np.zeros((M + 2, N + 2), order="F")
+    lib().orc_get_vv(_p(I2), C.c_int(M), C.c_int(N), _p(VV))
+    return VV
+
+
+def interp_cubic(VV: np.ndarray, M: int, N: int, Xq: float, Yq: float) -> float:
+    VV = _f64(VV)
+    return lib().orc_interp_cubic(_p(VV), M, N, float(Xq), float(Yq))
+
+
+def make_params(opts: dict, Mo: int, No: int) -> OrcParams:
+    """opts uses the reference option names plus the engine knobs of
+    gqmap_opticalflow_amd.options (engine, step0, ...)."""
+    sup = opts.get("engine", "mixture") == "super"
+    p = OrcParams()
+    p.Mo, p.No = Mo, No
+    p.M, p.N = (Mo // 4, No // 4) if sup else (Mo, No)
+    p.L, p.K = int(opts["L"]), int(opts["K"])
+    p.super_ = int(sup)
+    p.guard_a = int(opts.get("guard_a", not sup))
+    p.T = float(opts.get("temperature", 0.0))
+    p.drate = float(opts.get("drate", 0.5))
+    p.t_min = float(opts.get("t_min", 0.001))
+    p.t_decay_every = int(opts.get("t_decay_every", 500 if sup else 0))
+    p.epsn, p.lambdad, p.lambdas = float(opts["epsn"]), float(opts["lambdad"]), float(opts["lambdas"])
+    p.minu, p.maxu = float(opts["minu"]), float(opts["maxu"])
+    p.minv, p.maxv = float(opts["minv"]), float(opts["maxv"])
+    p.step0 = float(opts.get("step0", 0.001 if sup else 0.1))
+    p.step_decay = float(opts.get("step_decay", 4000.0 if sup else 8000.0))
+    p.sig_lo = float(opts.get("sig_lo", 0.01))
+    p.sig_hi = float(opts.get("sig_hi", 25.0 if sup else 23.0))
+    p.corr_tor = float(opts.get("corr_tor", 1 - 1e-5))
+    p.alpha_mode = int(opts.get("alpha_mode", 0))
+    p.alpha_start = int(opts.get("alpha_start", 500))
+    p.alpha_lr = float(opts.get("alpha_lr", 1e-7))
+    p.tor = float(opts.get("tor", 1e-4))
+    return p
+
+
+class State:
+    """Host copy of the engine state in MATLAB layout."""
+
+    def __init__(self, muu, muv, sigu, sigv, pn, rou, w, alpha):
+        self.muu, self.muv, self.sigu, self.sigv, self.pn = map(_f64, (muu, muv, sigu, sigv, pn))
+        self.rou = _f64(rou)
+        self.w, self.alpha = _f64(np.ravel(w)), _f64(np.ravel(alpha))
+
+    def copy(self):
+        return State(*(np.array(a, order="F", copy=True) for a in self.arrays()))
+
+    def arrays(self):
+        return (self.muu, self.muv, self.sigu, self.sigv, self.pn, self.rou, self.w, self.alpha)
+
+    def cstruct(self) -> OrcState:
+        s = OrcState()
+        for name, a in zip(("muu", "muv", "sigu", "sigv", "pn", "rou", "w", "alpha"), self.arrays()):
+            setattr(s, name, _p(a))
+        return s
+
+
+def run(opts: dict, I1: np.ndarray, I2: np.ndarray, state: State, it_first: int, n_iter: int,
+        T: float | None = None, nthreads: int = 0):
+    """Run n_iter iterations in place on `state`.  Returns (done, trace[done,3], T)."""
+    I1 = _f64(I1)
+    Mo, No = I1.shape
+    p = make_params(opts, Mo, No)
+    VV = get_vv(I2)
+    Tbox = (C.c_double * 1)(p.T if T is None else T)
+    trace = np.zeros((max(n_iter, 1), 3))
+    cs = state.cstruct()
+    done = lib().orc_run(C.byref(p), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
+                         _p(trace), nthreads)
+    return done, trace[:done].copy(), Tbox[0]
+
+
+def gradients(opts: dict, I1, I2, state: State, T: float | None = None, nthreads: int = 0):
+    I1 = _f64(I1)
+    Mo, No = I1.shape
+    p = make_params(opts, Mo, No)
+    VV = get_vv(I2)
+    MNL = p.M * p.N * p.L
+    node = np.zeros(7 * MNL); edge = np.zeros(7 * MNL * 4)
+    lib().orc_gradients(C.byref(p), _p(I1), _p(VV), C.byref(state.cstruct()),
+                        C.c_double(p.T if T is None else T), _p(node), _p(edge), nthreads)
+    return (node.reshape((p.M, p.N, p.L, 7), order="F"),
+            edge.reshape((p.M, p.N, p.L, 2, 2, 7), order="F"))
+
+
+def projsplx(y) -> np.ndarray:
+    y = _f64(np.asarray(y, dtype=np.float64).ravel())
+    x = np.zeros_like(y)
+    lib().orc_projsplx(_p(y), _p(x), C.c_int(y.size))
+    return x
+
+
+def flow_to_color(flow: np.ndarray, max_flow: float = 0.0):
+    flow = _f64(flow)
+    M, N, _ = flow.shape
+    img = np.zeros((M, N, 3), dtype=np.uint8, order="F")
+    flo = np.zeros((M, N, 2), order="F")
+    stats = np.zeros(4)
+    unk = np.zeros((M, N), dtype=np.uint8, order="F")
+    u8 = C.POINTER(C.c_ubyte)
+    lib().orc_flow_to_color(_p(flow), C.c_int(M), C.c_int(N), C.c_double(max_flow),
+                            img.ctypes.data_as(u8), _p(flo), _p(stats), unk.ctypes.data_as(u8))
+    return img, flo, stats, unk.astype(bool)
+
+
+def aepe(tflow, flow, unknown, r0: int = 1) -> float:
+    tflow, flow = _f64(tflow), _f64(flow)
+    unk = np.require(unknown, dtype=np.uint8, requirements=["F_CONTIGUOUS"])
+    M, N = unk.shape
+    f = lib().orc_aepe
+    f.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_ubyte),
+                  C.c_int, C.c_int, C.c_int]
+    return f(_p(tflow), _p(flow), unk.ctypes.data_as(C.POINTER(C.c_ubyte)), M, N, r0)
+
+
+def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0) -> np.ndarray:
+    muu, sigu, muv, sigv = map(_f64, (muu, sigu, muv, sigv))
+    alpha = _f64(np.ravel(alpha))
+    M, N, L = muu.shape
+    out = np.zeros((M, N, 2), order="F")
+    lib().orc_get_map(_p(alpha), _p(muu), _p(sigu), _p(muv), _p(sigv), M, N, L, _p(out),
+                      nthreads)
+    return out
