@@ -34,15 +34,42 @@
 
 #include "gqmap_internal.h"
 
+#pragma clang fp contract(off)
+
+namespace gq {
+// correctly rounded sqrt without the denormal rescaling: every argument is
+// eps + d^2 (eps > 0), 1 +- p (|p| < 1) or 1 - p^2, all far above 2^-767,
+// where LLVM's f64 sqrt sequence applies no scaling -- same bits as sqrt().
+__device__ __forceinline__ double gq_sqrt_dev(double x)
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+__device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x); }
+}  // namespace gq
+
+#define GQ_HD __device__ __forceinline__
+#define GQ_SQRT(x) gq::gq_sqrt_dev(x)
+#define GQ_UNROLL2 _Pragma("unroll 2")
+#include "gqmap_math.h"
+
 namespace gq {
 
 constexpr int TILE = 16;
 constexpr int BLOCK = TILE * TILE;
-constexpr int TS = 256;        // quadrature table stride (K2 <= 256)
+constexpr int TS = TAB_STRIDE;
 constexpr int NTAB = 8;        // xi, xj, w, w*xi, w*xj, w*(xi^2+xj^2), w*(xi^2-xj^2), w*xi*xj
 constexpr int NPLANES = 9;
 constexpr int TRACE_CAP = 8192;
 constexpr int GRAPH_CHUNK = 50;
+constexpr int NFIX = 4;        // fixed slots per block: Energy, sum|dmu_u|, sum|dsig_u|, #nonfinite
 
 struct Ctl {
     int it;    // next iteration (1-based)
@@ -62,7 +89,7 @@ struct IterParams {
     R *st1;
     const R *__restrict__ tab;  // NTAB x TS
     Ctl *ctl;
-    double *partials;           // nblocks x (3 + L)
+    fix128 *partials;           // nblocks x (NFIX + L)
     int M, N, Mo, No, M2, L, K2;
     int tiles_m, tiles_n;
     R epsn, lamd, lams;
@@ -71,80 +98,6 @@ struct IterParams {
     int guard;
     int64_t MNL;
 };
-
-// ---------------------------------------------------------------------------
-// device math
-// ---------------------------------------------------------------------------
-template <typename R>
-__device__ __forceinline__ void keys4(R t, R &w0, R &w1, R &w2, R &w3)
-{
-    // Keys a=-1/2 weights in the x2 form of node_pot (gqmap_gpu_mixture.m:167-174)
-    w0 = ((R(2) - t) * t - R(1)) * t;
-    w1 = (R(3) * t - R(5)) * t * t + R(2);
-    w2 = ((R(4) - R(3) * t) * t + R(1)) * t;
-    w3 = (t - R(1)) * t * t;
-}
-
-template <typename R>
-__device__ __forceinline__ R bicubic_cell(const R *__restrict__ c, int M2, R so, R to)
-{
-    R t0, t1, t2, t3, s0, s1, s2, s3;
-    keys4(to, t0, t1, t2, t3);
-    keys4(so, s0, s1, s2, s3);
-    const R v0 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
-    c += M2;
-    const R v1 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
-    c += M2;
-    const R v2 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
-    c += M2;
-    const R v3 = c[0] * t0 + c[1] * t1 + c[2] * t2 + c[3] * t3;
-    return (s0 * v0 + s1 * v1 + s2 * v2 + s3 * v3) * R(0.25);
-}
-
-// interp2-cubic sample at 1-based column jj + x1, row ii + x2 (node_pot, :157-176).
-// fp64 mirrors the reference arithmetic (Xq = j + x1, clamp, floor).
-__device__ __forceinline__ double sample(const double *__restrict__ VV, int M2, int Mo, int No,
-                                         int ii, int jj, double x1, double x2)
-{
-    const double Xq = fmin(fmax(jj + x1, 1.0), (double)No);
-    const double Yq = fmin(fmax(ii + x2, 1.0), (double)Mo);
-    const int ix = min((int)Xq, No - 1);  // Xq >= 1: truncation == floor
-    const int iy = min((int)Yq, Mo - 1);
-    return bicubic_cell(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, Xq - ix, Yq - iy);
-}
-// fp32: split the offset into integer + fraction relative to the pixel so the
-// fractional position keeps full precision at any image size.
-__device__ __forceinline__ float sample(const float *__restrict__ VV, int M2, int Mo, int No,
-                                        int ii, int jj, float x1, float x2)
-{
-    x1 = fminf(fmaxf(x1, float(1 - jj)), float(No - jj));
-    x2 = fminf(fmaxf(x2, float(1 - ii)), float(Mo - ii));
-    const float fx = floorf(x1), fy = floorf(x2);
-    float so = x1 - fx, to = x2 - fy;
-    int ix = jj + (int)fx, iy = ii + (int)fy;
-    if (ix > No - 1) { ix = No - 1; so = 1.f; }
-    if (iy > Mo - 1) { iy = Mo - 1; to = 1.f; }
-    return bicubic_cell(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, so, to);
-}
-
-// sqrt for arguments in [1e-300, 1e300] (every call site passes eps + d^2 or
-// 1 +- p with eps > 0, |p| < 1): the same rsq + Goldschmidt + two Newton
-// corrections LLVM emits for sqrt(double), minus its denormal rescaling.
-__device__ __forceinline__ double dsqrt(double x)
-{
-    const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y, h = 0.5 * y;
-    const double r = fma(-h, g, 0.5);
-    g = fma(g, r, g);
-    h = fma(h, r, h);
-    double d = fma(-g, g, x);
-    g = fma(d, h, g);
-    d = fma(-g, g, x);
-    return fma(d, h, g);
-}
-__device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
-__device__ __forceinline__ double dlog(double x) { return log(x); }
-__device__ __forceinline__ float dlog(float x) { return __logf(x); }
 
 // Quadrature tables are read with wave-uniform indices; routing them through
 // the constant address space turns every access into a scalar (SMEM) load.
@@ -156,137 +109,21 @@ __device__ __forceinline__ ctab_t<R> as_const(const R *p)
     return (ctab_t<R>)p;
 }
 
-template <typename R>
-struct Grad {
-    R da, du1, du2, do1, do2, dp, E;
-};
-
-// Basis sums of the quadrature: with f_k = WIWJ(k)*pot_k,
-//   S0=sum f, Sxi=sum f*XI, Sxj=sum f*XJ, Sa=sum f*(XI^2+XJ^2), Sm=sum f*(XI^2-XJ^2), Sx=sum f*XI*XJ
-// every accumulator of the reference (dp, du1, du2, do1, do2, Ei) is a fixed
-// linear combination of these six (gqmap_gpu_mixture.m:99-105).
-template <typename R>
-struct Sums {
-    R s0 = 0, sxi = 0, sxj = 0, sa = 0, sm = 0, sx = 0;
-    __device__ __forceinline__ void add(ctab_t<R> tab, int k, R f)
-    {
-        s0 = fma(tab[2 * TS + k], f, s0);
-        sxi = fma(tab[3 * TS + k], f, sxi);
-        sxj = fma(tab[4 * TS + k], f, sxj);
-        sa = fma(tab[5 * TS + k], f, sa);
-        sm = fma(tab[6 * TS + k], f, sm);
-        sx = fma(tab[7 * TS + k], f, sx);
-    }
-};
-
-// Epilogue shared by node (tau = -3T) and edge (tau = +T) gradients
-// (gqmap_gpu_mixture.m:107-115 and :137-145).  `lam` = -lambda (potential scale).
-template <typename R>
-__device__ __forceinline__ Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s,
-                                            R t, R tau, bool live)
+__device__ __forceinline__ fix128 shfl_xor_fix(fix128 v, int o)
 {
-    const R pi = R(M_PI), c1 = R(2.8378770664093454835606594728112);  // 1+log(2*pi)
-    const R S0 = lam * S.s0, Sxi = lam * S.sxi, Sxj = lam * S.sxj;
-    const R Sa = lam * S.sa, Sm = lam * S.sm, Sx = lam * S.sx;
-    const R pr = R(1) - p * p, sqrtpr = dsqrt(pr);
-    R dp = p * S0 - p * Sa + R(2) * Sx;
-    R du1 = (s - p * t) * Sxi + (t - p * s) * Sxj;
-    R du2 = (t - p * s) * Sxi + (s - p * t) * Sxj;
-    R do1 = Sa - S0 + Sm / sqrtpr;
-    R do2 = Sa - S0 - Sm / sqrtpr;
-    if (!live) dp = du1 = du2 = do1 = do2 = R(0);
-    Grad<R> g;
-    const R sq2 = R(M_SQRT2);
-    g.du1 = a * du1 * (sq2 / (o1 * pr)) / pi;
-    g.du2 = a * du2 * (sq2 / (o2 * pr)) / pi;
-    const R ent = tau != R(0) ? tau * (c1 + dlog(sqrtpr * o1 * o2)) : R(0);
-    g.da = S0 / pi + ent;
-    g.do1 = a * (do1 / pi + tau) / o1;
-    g.do2 = a * (do2 / pi + tau) / o2;
-    g.dp = a * (dp / pi - tau * p) / pr;
-    g.E = a * g.da;
-    return g;
+    const int64_t hi = (int64_t)(v >> 64);
+    const uint64_t lo = (uint64_t)v;
+    const int64_t h2 = __shfl_xor(hi, o, 64);
+    const uint64_t l2 = (uint64_t)__shfl_xor((int64_t)lo, o, 64);
+    return ((fix128)h2 << 64) | (fix128)l2;
 }
-
-template <typename R>
-__device__ __forceinline__ void spectral_st(R p, R &s, R &t)
-{
-    const R sp = dsqrt(R(1) + p), sm = dsqrt(R(1) - p);
-    s = (sp + sm) * R(0.5);
-    t = (sp - sm) * R(0.5);
-}
-
-// edge_grad_spectral (gqmap_gpu_mixture.m:118-146) with edge_pot (:180-182)
-template <typename R>
-__device__ __forceinline__ Grad<R> edge_grad(const IterParams<R> &P, R T, R a, R u1, R u2, R o1,
-                                             R o2, R p)
-{
-    R s, t;
-    spectral_st(p, s, t);
-    const R sq2 = R(M_SQRT2);
-    // x1 - x2 = sq2*o1*(s XI + t XJ) + u1 - sq2*o2*(t XI + s XJ) - u2
-    const R A = sq2 * (o1 * s - o2 * t), B = sq2 * (o1 * t - o2 * s), C = u1 - u2;
-    Sums<R> S;
-    const ctab_t<R> tab = as_const(P.tab);
-    const R eps = P.epsn;
-#pragma unroll 2
-    for (int k = 0; k < P.K2; ++k) {
-        const R d = fma(A, tab[k], fma(B, tab[TS + k], C));
-        S.add(tab, k, dsqrt(fma(d, d, eps)));
-    }
-    return epilogue(S, -P.lams, a, o1, o2, p, s, t, T, !P.guard || a != R(0));
-}
-
-// node_grad_spectral (gqmap_gpu_mixture.m:87-116; super: gqmap_gpuSuper_mix_entropy.m:87-122)
-template <typename R, bool SUPER>
-__device__ __forceinline__ Grad<R> node_grad(const IterParams<R> &P, R T, R a, R u1, R u2, R o1,
-                                             R o2, R p, int m, int n)
-{
-    R s, t;
-    spectral_st(p, s, t);
-    const R sq2 = R(M_SQRT2);
-    const R ax = sq2 * o1 * s, bx = sq2 * o1 * t;  // x1 = ax*XI + bx*XJ + u1
-    const R ay = sq2 * o2 * t, by = sq2 * o2 * s;  // x2 = ay*XI + by*XJ + u2
-    Sums<R> S;
-    const ctab_t<R> tab = as_const(P.tab);
-    const R eps = P.epsn;
-    if constexpr (!SUPER) {
-        const R I = P.I1[m + (int64_t)P.Mo * n];
-#pragma unroll 1
-        for (int k = 0; k < P.K2; ++k) {
-            const R x1 = fma(ax, tab[k], fma(bx, tab[TS + k], u1));
-            const R x2 = fma(ay, tab[k], fma(by, tab[TS + k], u2));
-            const R d = I - sample(P.VV, P.M2, P.Mo, P.No, m + 1, n + 1, x1, x2);
-            S.add(tab, k, dsqrt(fma(d, d, eps)));
-        }
-    } else {
-        R I[16];
-        const int i0 = 4 * m, j0 = 4 * n;  // 0-based top-left pixel of the 4x4 block
-#pragma unroll
-        for (int q = 0; q < 16; ++q) I[q] = P.I1[(i0 + (q & 3)) + (int64_t)P.Mo * (j0 + (q >> 2))];
-#pragma unroll 1
-        for (int k = 0; k < P.K2; ++k) {
-            const R x1 = fma(ax, tab[k], fma(bx, tab[TS + k], u1));
-            const R x2 = fma(ay, tab[k], fma(by, tab[TS + k], u2));
-            R f = 0;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const R d = I[q] - sample(P.VV, P.M2, P.Mo, P.No, i0 + (q & 3) + 1,
-                                          j0 + (q >> 2) + 1, x1, x2);
-                f += dsqrt(fma(d, d, eps));
-            }
-            S.add(tab, k, f);
-        }
-    }
-    return epilogue(S, -P.lamd, a, o1, o2, p, s, t, R(-3) * T, !P.guard || a != R(0));
-}
-
-__device__ __forceinline__ double wave_sum(double v)
+__device__ __forceinline__ fix128 wave_sum_fix(fix128 v)
 {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    for (int o = 32; o > 0; o >>= 1) v += shfl_xor_fix(v, o);
     return v;
 }
+__device__ __forceinline__ bool finite_d(double x) { return (bits_of(x) & 0x7ff0000000000000ULL) != 0x7ff0000000000000ULL; }
 
 // ---------------------------------------------------------------------------
 // fused iteration kernel
@@ -304,14 +141,14 @@ __global__ __launch_bounds__(BLOCK) void k_iter(IterParams<R> P)
     const R step = R(P.step0 / (1.0 + it / P.step_decay));
 
     // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin
-    // dispatch), so give each XCD a contiguous band of tiles (L2 locality of
-    // the VV gathers).  Speed only; correctness never depends on placement.
+    // dispatch), so each XCD gets a contiguous band of tiles (L2 locality of
+    // the VV gathers).  Speed only; results never depend on placement.
     const int nb = P.tiles_m * P.tiles_n;
     const int b = blockIdx.x;
     int tile = b >> 3;
     {
         const int xcd = b & 7;
-        for (int y = 0; y < xcd; ++y) tile += (nb - y + 7) >> 3;  // blocks owned by XCD groups < xcd
+        for (int y = 0; y < xcd; ++y) tile += (nb - y + 7) >> 3;
     }
     const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
     const int tid = threadIdx.x;
@@ -319,41 +156,43 @@ __global__ __launch_bounds__(BLOCK) void k_iter(IterParams<R> P)
     const int m0 = tm * TILE, n0 = tn * TILE;
     const int m = m0 + lm, n = n0 + ln;
     const int M = P.M, N = P.N;
-    const int64_t MNL = P.MNL;
+    const int64_t MNL = P.MNL, MN = (int64_t)M * N;
     const bool valid = m < M && n < N;
     auto interior = [&](int mm, int nn) { return mm >= 1 && mm <= M - 2 && nn >= 1 && nn <= N - 2; };
     const bool inner = valid && interior(m, n);
+    const ctab_t<R> tab = as_const(P.tab);
 
-    // in_up[uv][q][ln][lm]: du2/do2 of the edge from (m-1,n); in_left: from (m,n-1)
+    // in_up[uv][q][ln*16+lm]: du2/do2 of the edge from (m-1,n); in_left: from (m,n-1)
     __shared__ R in_up[2][2][BLOCK];
     __shared__ R in_left[2][2][BLOCK];
-    __shared__ double red[4][8];
+    __shared__ fix128 red[GQMAP_LMAX + NFIX][4];
 
-    double acc_E = 0, acc_mu = 0, acc_sg = 0;
-    double acc_da[GQMAP_LMAX];
-#pragma unroll
-    for (int l = 0; l < GQMAP_LMAX; ++l) acc_da[l] = 0;
+    fix128 fE = 0, fmu = 0, fsg = 0;
+    int nonfinite = 0;
+    const int wave = tid >> 6, lane = tid & 63;
 
     for (int l = 0; l < P.L; ++l) {
         const R a = R(ctl->alpha[l]);
-        const int64_t i = m + (int64_t)M * n + MNL * l;
+        const int64_t i = m + (int64_t)M * n + MN * l;
         R own[NPLANES];
 #pragma unroll
         for (int q = 0; q < NPLANES; ++q) own[q] = valid ? src[i + MNL * q] : R(0);
         Grad<R> nd{};
-        if (inner) nd = node_grad<R, SUPER>(P, T, a, own[0], own[1], own[2], own[3], own[4], m, n);
+        if (inner)
+            nd = node_grad<SUPER, R>(tab, P.K2, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, P.lamd,
+                                     P.guard != 0, T, a, own[0], own[1], own[2], own[3], own[4], m, n);
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
         // edges, then job 4: wave 0 recomputes the 64 halo edges entering
         // the tile from the row above / the column to the left.  One edge
         // body, streamed into accumulators and LDS, keeps VGPRs low.
-        R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1/do1
+        R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
-        double eacc = 0, dacc = 0;
+        R eE = 0, eda = 0;                                     // sum over the 4 edges
         const int njobs = tid < 64 ? 5 : 4;  // wave-uniform
 #pragma unroll 1
         for (int e = 0; e < njobs; ++e) {
             int dir, uv, hm, hn, rm, rn;
-            bool own_edge = e < 4;
+            const bool own_edge = e < 4;
             if (own_edge) {
                 dir = e & 1; uv = e >> 1;
                 hm = m; hn = n;
@@ -367,25 +206,25 @@ __global__ __launch_bounds__(BLOCK) void k_iter(IterParams<R> P)
                 rm = top ? m0 : hm;         rn = top ? hn : n0;
             }
             const bool r_inner = rm < M && rn < N && interior(rm, rn);
-            const bool need = own_edge ? (inner || (valid && r_inner))
-                                       : (hm >= 0 && hn >= 0 && r_inner);
+            const bool need = own_edge ? (inner || (valid && r_inner)) : (hm >= 0 && hn >= 0 && r_inner);
             Grad<R> g{};
             if (need) {
-                const int64_t h = hm + (int64_t)M * hn + MNL * l;
-                const int64_t r = rm + (int64_t)M * rn + MNL * l;
+                const int64_t h = hm + (int64_t)M * hn + MN * l;
+                const int64_t r = rm + (int64_t)M * rn + MN * l;
                 const R u1 = own_edge ? (uv ? own[1] : own[0]) : src[h + MNL * uv];
                 const R o1 = own_edge ? (uv ? own[3] : own[2]) : src[h + MNL * (2 + uv)];
                 const R p = own_edge ? (e == 0 ? own[5] : e == 1 ? own[6] : e == 2 ? own[7] : own[8])
                                      : src[h + MNL * (5 + dir + 2 * uv)];
-                g = edge_grad(P, T, a, u1, src[r + MNL * uv], o1, src[r + MNL * (2 + uv)], p);
+                g = edge_grad<R>(tab, P.K2, P.epsn, P.lams, P.guard != 0, T, a, u1,
+                                 src[r + MNL * uv], o1, src[r + MNL * (2 + uv)], p);
             }
             if (own_edge) {
-                if (uv == 0) { sum_mu0 += g.du1; sum_sg0 += g.do1; }
-                else         { sum_mu1 += g.du1; sum_sg1 += g.do1; }
+                if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
+                else         { sum_mu1 = sum_mu1 + g.du1; sum_sg1 = sum_sg1 + g.do1; }
                 if (e == 0) drou0 = g.dp; else if (e == 1) drou1 = g.dp;
                 else if (e == 2) drou2 = g.dp; else drou3 = g.dp;
-                eacc += (double)g.E;
-                dacc += (double)g.da;
+                eE = eE + g.E;
+                eda = eda + g.da;
                 // neighbour share: (m+1,n) reads in_up, (m,n+1) reads in_left
                 if (dir == 0 && lm + 1 < TILE) { in_up[uv][0][tid + 1] = g.du2; in_up[uv][1][tid + 1] = g.do2; }
                 if (dir == 1 && ln + 1 < TILE) { in_left[uv][0][tid + TILE] = g.du2; in_left[uv][1][tid + TILE] = g.do2; }
@@ -396,12 +235,13 @@ __global__ __launch_bounds__(BLOCK) void k_iter(IterParams<R> P)
             }
         }
         __syncthreads();
+        fix128 fda = 0;
         if (inner) {
             // dmuu = dmuu + sum(dmu1(:,:,:,:,1),4) + circshift(dmu2(..1,1),1) + circshift(dmu2(..2,1),1,2)
-            const R gmu_u = nd.du1 + sum_mu0 + in_up[0][0][tid] + in_left[0][0][tid];
-            const R gmu_v = nd.du2 + sum_mu1 + in_up[1][0][tid] + in_left[1][0][tid];
-            const R gsg_u = nd.do1 + sum_sg0 + in_up[0][1][tid] + in_left[0][1][tid];
-            const R gsg_v = nd.do2 + sum_sg1 + in_up[1][1][tid] + in_left[1][1][tid];
+            const R gmu_u = ((nd.du1 + sum_mu0) + in_up[0][0][tid]) + in_left[0][0][tid];
+            const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][tid]) + in_left[1][0][tid];
+            const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][tid]) + in_left[0][1][tid];
+            const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][tid]) + in_left[1][1][tid];
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
             dst[i + MNL * 0] = cl(own[0] + gmu_u * step, P.minu, P.maxu);
             dst[i + MNL * 1] = cl(own[1] + gmu_v * step, P.minv, P.maxv);
@@ -412,36 +252,44 @@ __global__ __launch_bounds__(BLOCK) void k_iter(IterParams<R> P)
             dst[i + MNL * 6] = cl(own[6] + drou1 * step, -P.corr, P.corr);
             dst[i + MNL * 7] = cl(own[7] + drou2 * step, -P.corr, P.corr);
             dst[i + MNL * 8] = cl(own[8] + drou3 * step, -P.corr, P.corr);
-            acc_E += (double)nd.E + eacc;
-            const double dal = (double)nd.da + dacc;
-#pragma unroll
-            for (int q = 0; q < GQMAP_LMAX; ++q)
-                if (q == l) acc_da[q] += dal;
-            acc_mu += fabs((double)gmu_u);
-            acc_sg += fabs((double)gsg_u);
+            // per-node contributions to the global sums (exact fixed point)
+            const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
+            const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
+            nonfinite += !finite_d(cE) + !finite_d(cda) + !finite_d(cmu) + !finite_d(csg);
+            fE += to_fix(cE);
+            fda = to_fix(cda);
+            fmu += to_fix(cmu);
+            fsg += to_fix(csg);
+        }
+        if (P.L > 1) {  // dalpha(l): only consumed by the alpha update
+            fda = wave_sum_fix(fda);
+            if (lane == 0) red[NFIX + l][wave] = fda;
         }
         __syncthreads();  // LDS reuse by the next component
     }
 
-    // block partials: Energy, sum|dmu_u|, sum|dsigma_u|, dalpha[0..L-1]
-    const int NP = 3 + P.L;
-    const int wave = tid >> 6, lane = tid & 63;
-    double* out = P.partials + (int64_t)blockIdx.x * NP;
-    for (int q = 0; q < NP; ++q) {
-        double v = q == 0 ? acc_E : q == 1 ? acc_mu : q == 2 ? acc_sg : 0.0;
-#pragma unroll
-        for (int l = 0; l < GQMAP_LMAX; ++l)
-            if (q == 3 + l) v = acc_da[l];
-        v = wave_sum(v);
-        if (lane == 0) red[wave][q & 7] = v;
-        __syncthreads();
-        if (tid == 0) out[q] = (red[0][q & 7] + red[1][q & 7]) + (red[2][q & 7] + red[3][q & 7]);
-        __syncthreads();
+    // block partials: Energy, sum|dmu_u|, sum|dsigma_u|, #nonfinite, dalpha[0..L-1]
+    fE = wave_sum_fix(fE);
+    fmu = wave_sum_fix(fmu);
+    fsg = wave_sum_fix(fsg);
+    fix128 fnf = wave_sum_fix((fix128)nonfinite);
+    if (lane == 0) {
+        red[0][wave] = fE;
+        red[1][wave] = fmu;
+        red[2][wave] = fsg;
+        red[3][wave] = fnf;
+    }
+    __syncthreads();
+    const int NP = NFIX + P.L;
+    if (tid < NP) {
+        fix128 v = 0;
+        if (tid < NFIX || P.L > 1) v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
+        P.partials[(int64_t)blockIdx.x * NP + tid] = v;
     }
 }
 
 struct FinParams {
-    const double *partials;
+    const fix128 *partials;
     int nblocks, L;
     Ctl *ctl;
     double *trace;     // TRACE_CAP x 3
@@ -457,12 +305,12 @@ __global__ __launch_bounds__(256) void k_finalize(FinParams F)
 {
     Ctl *ctl = F.ctl;
     if (ctl->stop) return;
-    __shared__ double sh[256];
-    __shared__ double tot[3 + GQMAP_LMAX];
-    const int NP = 3 + F.L;
+    __shared__ fix128 sh[256];
+    __shared__ double tot[NFIX + GQMAP_LMAX];
+    const int NP = NFIX + F.L;
     const int tid = threadIdx.x;
     for (int q = 0; q < NP; ++q) {
-        double v = 0;
+        fix128 v = 0;
         for (int b = tid; b < F.nblocks; b += 256) v += F.partials[(int64_t)b * NP + q];
         sh[tid] = v;
         __syncthreads();
@@ -470,29 +318,34 @@ __global__ __launch_bounds__(256) void k_finalize(FinParams F)
             if (tid < s) sh[tid] += sh[tid + s];
             __syncthreads();
         }
-        if (tid == 0) tot[q] = sh[0];
+        if (tid == 0) tot[q] = from_fix(sh[0]);
         __syncthreads();
     }
     if (tid != 0) return;
     const int it = ctl->it;
     const double step = F.step0 / (1.0 + it / F.step_decay);
-    const double energy = tot[0], ptdmu = tot[1] / F.count, ptdsig = tot[2] / F.count;
+    const bool bad = tot[3] != 0.0;  // a NaN/Inf contribution poisons the sums
+    const double nan = __builtin_nan("");
+    const double energy = bad ? nan : tot[0];
+    const double ptdmu = bad ? nan : tot[1] / F.count, ptdsig = bad ? nan : tot[2] / F.count;
     const int L = F.L;
     if (it > F.alpha_start && L != 1) {
+        double dal[GQMAP_LMAX];
+        for (int l = 0; l < L; ++l) dal[l] = bad ? nan : tot[NFIX + l];
         if (F.alpha_mode == GQMAP_ALPHA_SOFTMAX) {  // updateAlpha, gqmap_gpu_mixture.m:78-86
             double sda = 0;
-            for (int l = 0; l < L; ++l) sda += tot[3 + l] * ctl->alpha[l];
+            for (int l = 0; l < L; ++l) sda = sda + dal[l] * ctl->alpha[l];
             double se = 0, ew[GQMAP_LMAX];
             for (int l = 0; l < L; ++l) {
-                const double dw = ctl->alpha[l] * (tot[3 + l] - sda);
+                const double dw = ctl->alpha[l] * (dal[l] - sda);
                 ctl->w[l] = fmin(fmax(ctl->w[l] + dw * step * F.alpha_lr, -300.0), 300.0);
-                ew[l] = exp(ctl->w[l]);
-                se += ew[l];
+                ew[l] = gq_exp(ctl->w[l]);
+                se = se + ew[l];
             }
             for (int l = 0; l < L; ++l) ctl->alpha[l] = ew[l] / se;
         } else {  // projsplx(alpha + dalpha*step*lr), projsplx.m:15-30
             double y[GQMAP_LMAX], s[GQMAP_LMAX];
-            for (int l = 0; l < L; ++l) s[l] = y[l] = ctl->alpha[l] + tot[3 + l] * step * F.alpha_lr;
+            for (int l = 0; l < L; ++l) s[l] = y[l] = ctl->alpha[l] + dal[l] * step * F.alpha_lr;
             for (int i = 1; i < L; ++i) {
                 double v = s[i];
                 int j = i;
@@ -502,7 +355,7 @@ __global__ __launch_bounds__(256) void k_finalize(FinParams F)
             double tmpsum = 0, tmax = 0;
             bool bget = false;
             for (int ii = 0; ii < L - 1; ++ii) {
-                tmpsum += s[ii];
+                tmpsum = tmpsum + s[ii];
                 tmax = (tmpsum - 1) / (ii + 1);
                 if (tmax >= s[ii + 1]) { bget = true; break; }
             }
@@ -526,7 +379,7 @@ __global__ void k_init_state(R *st0, R *st1, int64_t MNL, uint64_t b1, uint64_t 
 {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= MNL) return;
-    // gqmap_gpu_mixture.m:19-24
+    // gqmap_gpu_mixture.m:19-24 (no contraction: same bits as the host formula)
     const R v[NPLANES] = {R(minu + u01(b1, i) * (maxu - minu)), R(minv + u01(b2, i) * (maxv - minv)),
                           R(u01(b3, i) + (maxu - minu)),        R(u01(b4, i) + (maxv - minv)),
                           R(0), R(0), R(0), R(0), R(0)};
@@ -535,6 +388,13 @@ __global__ void k_init_state(R *st0, R *st1, int64_t MNL, uint64_t b1, uint64_t 
         st0[i + MNL * q] = v[q];
         st1[i + MNL * q] = v[q];
     }
+}
+
+__device__ __forceinline__ double wave_sum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
 // profile_logP (gqmap_gpu_mixture.m:148-154; super :152-169): per-block partials.
@@ -551,13 +411,13 @@ __global__ __launch_bounds__(256) void k_logp(IterParams<R> P, const R *__restri
             const R u = map[i], w = map[i + MN];
             if constexpr (!SUPER) {
                 const R d = P.I1[m + (int64_t)P.Mo * n] - sample(P.VV, P.M2, P.Mo, P.No, m + 1, n + 1, u, w);
-                v += (double)(-P.lamd * dsqrt(P.epsn + d * d));
+                v += (double)(-P.lamd * gq_sqrt_dev(P.epsn + d * d));
             } else {
                 for (int q = 0; q < 16; ++q) {
-                    const int ii = 4 * m + (q & 3), jj = 4 * n + (q >> 2);
+                    const int ii = 4 * m + (q >> 2), jj = 4 * n + (q & 3);
                     const R d = P.I1[ii + (int64_t)P.Mo * jj] -
                                 sample(P.VV, P.M2, P.Mo, P.No, ii + 1, jj + 1, u, w);
-                    v += (double)(-P.lamd * dsqrt(P.epsn + d * d));
+                    v += (double)(-P.lamd * gq_sqrt_dev(P.epsn + d * d));
                 }
             }
             // edge_pot(cat(4,uv,uv), cat(4,circshift(uv,-1),circshift(uv,-1,2)))
@@ -566,8 +426,8 @@ __global__ __launch_bounds__(256) void k_logp(IterParams<R> P, const R *__restri
             for (int c = 0; c < 2; ++c) {
                 const R x = map[i + MN * c];
                 const R dd = x - map[jd + MN * c], dr = x - map[jr + MN * c];
-                v += (double)(-P.lams * dsqrt(P.epsn + dd * dd));
-                v += (double)(-P.lams * dsqrt(P.epsn + dr * dr));
+                v += (double)(-P.lams * gq_sqrt_dev(P.epsn + dd * dd));
+                v += (double)(-P.lams * gq_sqrt_dev(P.epsn + dr * dr));
             }
         }
     }
@@ -576,6 +436,15 @@ __global__ __launch_bounds__(256) void k_logp(IterParams<R> P, const R *__restri
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// math self-test (not part of the public ABI): fn 0 sqrt, 1 log, 2 exp
+__global__ void k_selftest(int fn, const double *in, double *out, int64_t n)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = in[i];
+    out[i] = fn == 0 ? gq_sqrt_dev(x) : fn == 1 ? gq_log(x) : gq_exp(x);
 }
 
 }  // namespace gq
@@ -600,7 +469,8 @@ struct gqmap_ctx {
     size_t rsz = 8;
     void *d_VV = nullptr, *d_I1 = nullptr, *d_st[2] = {nullptr, nullptr}, *d_tab = nullptr;
     Ctl *d_ctl = nullptr;
-    double *d_partials = nullptr, *d_trace = nullptr;
+    fix128 *d_partials = nullptr;
+    double *d_trace = nullptr;
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     bool have_images = false, have_state = false;
     hipGraphExec_t graph = nullptr;
@@ -622,7 +492,7 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     }
     if (c->d_partials) (void)hipFree(c->d_partials);
     c->d_partials = nullptr;
-    GQ_HIP(hipMalloc(&c->d_partials, sizeof(double) * (size_t)c->nblocks * (3 + c->L) + 64));
+    GQ_HIP(hipMalloc((void **)&c->d_partials, sizeof(fix128) * (size_t)c->nblocks * (NFIX + c->L) + 64));
     return GQMAP_OK;
 }
 
@@ -1164,6 +1034,22 @@ gqmap_status gqmap_log_p(gqmap_ctx *c, const double *map, double *logp)
     return s;
 }
 
+// Not in the public header: device math self-test used by tests/ (fn 0 sqrt,
+// 1 log, 2 exp) to pin the device primitives against the host ones.
+int gqmap_selftest_math(int fn, const double *in, double *out, int64_t n)
+{
+    double *d = nullptr;
+    if (hipMalloc(&d, sizeof(double) * 2 * n) != hipSuccess) return GQMAP_ERR_HIP;
+    hipError_t e = hipMemcpy(d, in, sizeof(double) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        k_selftest<<<(int)((n + 255) / 256), 256>>>(fn, d, d + n, n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, d + n, sizeof(double) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? GQMAP_OK : GQMAP_ERR_HIP;
+}
+
 gqmap_status gqmap_synchronize(gqmap_ctx *c)
 {
     clear_error();
@@ -1179,7 +1065,7 @@ void gqmap_destroy(gqmap_ctx *c)
     DeviceGuard dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graph(c);
-    void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, c->d_partials, c->d_trace};
+    void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);

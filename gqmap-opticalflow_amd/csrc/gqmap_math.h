@@ -1,0 +1,336 @@
+// gqmap_math.h -- per-element arithmetic of one QGMAP iteration.
+//
+// This header is the arithmetic specification of the hot path: the HIP
+// kernel (gqmap_engine.hip) and the CPU emulator (oracle/gqmap_emul.cpp,
+// test infrastructure) both include it, so a node/edge gradient evaluates to
+// the same bits on both sides.  Rules that make that hold:
+//   * every fused multiply-add is an explicit fma(); both sides compile with
+//     -ffp-contract=off, so nothing else is contracted;
+//   * sqrt and division are IEEE correctly rounded on both sides
+//     (GQ_SQRT is provided by the includer: the device form is LLVM's
+//     correctly rounded f64 sequence without its denormal rescaling);
+//   * log/exp are the deterministic routines below (no libm);
+//   * sums over pixels are exact (128-bit fixed point), so their value does
+//     not depend on the order in which tiles, waves or threads add them.
+//
+// The includer defines GQ_HD (e.g. `__device__ __forceinline__` or `inline`),
+// GQ_SQRT(x) for double and float and GQ_UNROLL2 (a loop-unroll pragma or
+// nothing), makes fma/fmin/fmax/floorf/fminf/fmaxf visible for float and double, then includes
+// this file.
+//
+// Reference lines this arithmetic restates: node_pot / edge_pot
+// (gqmap_gpu_mixture.m:156-182), node/edge_grad_spectral (:87-146), super
+// node sum (gqmap_gpuSuper_mix_entropy.m:94-105).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+namespace gq {
+
+#ifndef GQ_M_PI
+#define GQ_M_PI 3.14159265358979323846
+#define GQ_M_SQRT2 1.41421356237309504880
+#endif
+
+constexpr int TAB_STRIDE = 256;  // quadrature table stride (K2 <= 256)
+
+// ---------------------------------------------------------------------------
+// deterministic log / exp (classic fdlibm-style reductions, < 1 ulp)
+// ---------------------------------------------------------------------------
+GQ_HD uint64_t bits_of(double x)
+{
+    uint64_t u;
+    memcpy(&u, &x, 8);
+    return u;
+}
+GQ_HD double from_bits(uint64_t u)
+{
+    double x;
+    memcpy(&x, &u, 8);
+    return x;
+}
+
+// natural log for positive normal x (callers pass sqrt(1-p^2)*o1*o2 > 0)
+GQ_HD double gq_log(double x)
+{
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+                 Lg7 = 1.479819860511658591e-01;
+    uint64_t u = bits_of(x);
+    int k = (int)((u >> 52) & 0x7ff) - 1023;
+    u = (u & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL;  // m in [1,2)
+    double m = from_bits(u);
+    if (m > 1.4142135623730951) {
+        m = m * 0.5;
+        k += 1;
+    }
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double z = s * s, w = z * z;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const double R = t2 + t1;
+    const double hfsq = 0.5 * f * f;
+    const double dk = (double)k;
+    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+// exp for |x| <= 700 (softmax of w in [-300,300]; normal pdf tails flush to 0)
+GQ_HD double gq_exp(double x)
+{
+    if (x < -745.0) return 0.0;
+    if (x > 709.0) x = 709.0;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 inv_ln2 = 1.44269504088896338700e+00;
+    const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+                 P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+                 P5 = 4.13813679705723846039e-08;
+    const double kd = x * inv_ln2 + (x < 0 ? -0.5 : 0.5);
+    const int k = (int)kd;  // round half away from zero
+    const double hi = x - (double)k * ln2_hi, lo = (double)k * ln2_lo;
+    const double r = hi - lo;
+    const double t = r * r;
+    const double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+    const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+    // y * 2^k, split so subnormal results are exact scalings
+    int k1 = k / 2, k2 = k - k1;
+    return y * from_bits((uint64_t)(1023 + k1) << 52) * from_bits((uint64_t)(1023 + k2) << 52);
+}
+
+GQ_HD double gq_logf_via_double(float x) { return gq_log((double)x); }
+
+template <typename R>
+GQ_HD R gq_logr(R x);
+template <>
+GQ_HD double gq_logr<double>(double x) { return gq_log(x); }
+template <>
+GQ_HD float gq_logr<float>(float x) { return (float)gq_log((double)x); }
+
+// ---------------------------------------------------------------------------
+// exact, order-independent sums: value * 2^64 as a 128-bit integer
+// ---------------------------------------------------------------------------
+typedef __int128 fix128;
+
+GQ_HD fix128 to_fix(double x)
+{
+    // x = mant * 2^(exp-1075) with a 53-bit integer mantissa (normal doubles)
+    const uint64_t u = bits_of(x);
+    const int bexp = (int)((u >> 52) & 0x7ff);
+    if (bexp == 0x7ff) return (fix128)0;  // inf/nan: excluded (flagged separately)
+    int64_t mant = (int64_t)(u & 0x000fffffffffffffULL);
+    int e = bexp - 1075;
+    if (bexp) mant |= (int64_t)1 << 52;
+    else e = -1074;
+    const int shift = e + 64;  // scale by 2^64
+    fix128 v;
+    if (shift >= 0) {
+        const int s = shift > 72 ? 72 : shift;  // saturate |x| >= 2^61
+        v = (fix128)mant << s;
+    } else if (shift > -64) {
+        v = (fix128)(mant >> (-shift));  // truncation toward zero of |x|
+    } else {
+        v = 0;
+    }
+    return (u >> 63) ? -v : v;
+}
+
+GQ_HD double from_fix(fix128 v)
+{
+    const int64_t hi = (int64_t)(v >> 64);
+    const uint64_t lo = (uint64_t)v;
+    return (double)hi + (double)lo * 5.42101086242752217004e-20;  // lo * 2^-64
+}
+
+// ---------------------------------------------------------------------------
+// interpolation (node_pot, gqmap_gpu_mixture.m:157-176)
+// ---------------------------------------------------------------------------
+template <typename R>
+GQ_HD void keys4(R t, R &w0, R &w1, R &w2, R &w3)
+{
+    // Keys a=-1/2 weights in the x2 form of the reference
+    const R t2 = t * t;
+    w0 = fma(R(2) - t, t, R(-1)) * t;         // ((2-t)t - 1)t
+    w1 = fma(fma(R(3), t, R(-5)), t2, R(2));  // (3t-5)t^2 + 2
+    w2 = fma(fma(R(-3), t, R(4)), t, R(1)) * t;  // ((4-3t)t + 1)t
+    w3 = (t - R(1)) * t2;                     // (t-1)t^2
+}
+
+template <typename R, typename VP>
+GQ_HD R bicubic_cell(VP c, int M2, R so, R to)
+{
+    R t0, t1, t2, t3, s0, s1, s2, s3;
+    keys4(to, t0, t1, t2, t3);
+    keys4(so, s0, s1, s2, s3);
+    const R v0 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    c += M2;
+    const R v1 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    c += M2;
+    const R v2 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    c += M2;
+    const R v3 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0))) * R(0.25);
+}
+
+// interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV.
+// fp64: the reference's own position arithmetic (Xq = j + x1, clamp, floor).
+template <typename VP>
+GQ_HD double sample(VP VV, int M2, int Mo, int No, int ii, int jj, double x1, double x2)
+{
+    // min(max(.,1),N) with MATLAB's NaN-ignoring max/min (IEEE maxNum/minNum)
+    const double Xq = fmin(fmax((double)jj + x1, 1.0), (double)No);
+    const double Yq = fmin(fmax((double)ii + x2, 1.0), (double)Mo);
+    int ix = (int)Xq, iy = (int)Yq;  // Xq >= 1: truncation == floor
+    ix = ix > No - 1 ? No - 1 : ix;
+    iy = iy > Mo - 1 ? Mo - 1 : iy;
+    return bicubic_cell<double>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, Xq - (double)ix,
+                                Yq - (double)iy);
+}
+// fp32: integer + fraction relative to the pixel, so the fractional position
+// keeps full precision at any image size.
+template <typename VP>
+GQ_HD float sample(VP VV, int M2, int Mo, int No, int ii, int jj, float x1, float x2)
+{
+    const float lox = (float)(1 - jj), hix = (float)(No - jj);
+    const float loy = (float)(1 - ii), hiy = (float)(Mo - ii);
+    x1 = fminf(fmaxf(x1, lox), hix);
+    x2 = fminf(fmaxf(x2, loy), hiy);
+    const float fx = floorf(x1), fy = floorf(x2);
+    float so = x1 - fx, to = x2 - fy;
+    int ix = jj + (int)fx, iy = ii + (int)fy;
+    if (ix > No - 1) { ix = No - 1; so = 1.f; }
+    if (iy > Mo - 1) { iy = Mo - 1; to = 1.f; }
+    return bicubic_cell<float>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, so, to);
+}
+
+// ---------------------------------------------------------------------------
+// spectral quadrature of the node / edge potentials
+// ---------------------------------------------------------------------------
+template <typename R>
+struct Grad {
+    R da, du1, du2, do1, do2, dp, E;
+};
+
+// Basis sums: with f_k the potential at quadrature point k and table
+// weights W_k = WIWJ(k),
+//   s0 = sum W f, sxi = sum W XI f, sxj = sum W XJ f,
+//   sa = sum W (XI^2+XJ^2) f, sm = sum W (XI^2-XJ^2) f, sx = sum W XI XJ f.
+// Every accumulator of the reference (dp, du1, du2, do1, do2, Ei;
+// gqmap_gpu_mixture.m:99-105) is a fixed linear combination of these six.
+// Table rows: 0 XI, 1 XJ, 2 W, 3 W XI, 4 W XJ, 5 W(XI^2+XJ^2), 6 W(XI^2-XJ^2), 7 W XI XJ.
+template <typename R>
+struct Sums {
+    R s0 = 0, sxi = 0, sxj = 0, sa = 0, sm = 0, sx = 0;
+    template <typename TP>
+    GQ_HD void add(TP tab, int k, R f)
+    {
+        s0 = fma(tab[2 * TAB_STRIDE + k], f, s0);
+        sxi = fma(tab[3 * TAB_STRIDE + k], f, sxi);
+        sxj = fma(tab[4 * TAB_STRIDE + k], f, sxj);
+        sa = fma(tab[5 * TAB_STRIDE + k], f, sa);
+        sm = fma(tab[6 * TAB_STRIDE + k], f, sm);
+        sx = fma(tab[7 * TAB_STRIDE + k], f, sx);
+    }
+};
+
+template <typename R>
+GQ_HD void spectral_st(R p, R &s, R &t)
+{
+    const R sp = GQ_SQRT(R(1) + p), sm = GQ_SQRT(R(1) - p);
+    s = (sp + sm) * R(0.5);
+    t = (sp - sm) * R(0.5);
+}
+
+// Epilogue shared by node (tau = -3T) and edge (tau = +T) gradients
+// (gqmap_gpu_mixture.m:107-115 and :137-145).  lam = -lambda scales the sums.
+template <typename R>
+GQ_HD Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s, R t, R tau,
+                       bool live)
+{
+    const R pi = R(GQ_M_PI);
+    const R c1 = R(2.8378770664093454835606594728112);  // 1 + log(2*pi)
+    const R S0 = lam * S.s0, Sxi = lam * S.sxi, Sxj = lam * S.sxj;
+    const R Sa = lam * S.sa, Sm = lam * S.sm, Sx = lam * S.sx;
+    const R pr = R(1) - p * p;
+    const R sqrtpr = GQ_SQRT(pr);
+    const R a1 = s - p * t, a2 = t - p * s;
+    R dp = p * (S0 - Sa) + R(2) * Sx;
+    R du1 = a1 * Sxi + a2 * Sxj;
+    R du2 = a2 * Sxi + a1 * Sxj;
+    const R smr = Sm / sqrtpr;
+    R do1 = (Sa - S0) + smr;
+    R do2 = (Sa - S0) - smr;
+    if (!live) dp = du1 = du2 = do1 = do2 = R(0);
+    Grad<R> g;
+    const R sq2 = R(GQ_M_SQRT2);
+    g.du1 = a * du1 * (sq2 / (o1 * pr)) / pi;
+    g.du2 = a * du2 * (sq2 / (o2 * pr)) / pi;
+    const R ent = tau != R(0) ? tau * (c1 + gq_logr<R>(sqrtpr * o1 * o2)) : R(0);
+    g.da = S0 / pi + ent;
+    g.do1 = a * (do1 / pi + tau) / o1;
+    g.do2 = a * (do2 / pi + tau) / o2;
+    g.dp = a * (dp / pi - tau * p) / pr;
+    g.E = a * g.da;
+    return g;
+}
+
+// edge_grad_spectral (gqmap_gpu_mixture.m:118-146) with edge_pot (:180-182):
+// x1 - x2 = sqrt2*o1*(s XI + t XJ) + u1 - sqrt2*o2*(t XI + s XJ) - u2
+template <typename R, typename TP>
+GQ_HD Grad<R> edge_grad(TP tab, int K2, R eps, R lams, bool guard, R T, R a, R u1, R u2, R o1,
+                        R o2, R p)
+{
+    R s, t;
+    spectral_st(p, s, t);
+    const R sq2 = R(GQ_M_SQRT2);
+    const R A = sq2 * (o1 * s - o2 * t), B = sq2 * (o1 * t - o2 * s), C = u1 - u2;
+    Sums<R> S;
+    GQ_UNROLL2
+    for (int k = 0; k < K2; ++k) {
+        const R d = fma(A, tab[k], fma(B, tab[TAB_STRIDE + k], C));
+        S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+    }
+    return epilogue(S, -lams, a, o1, o2, p, s, t, T, !guard || a != R(0));
+}
+
+// node_grad_spectral (gqmap_gpu_mixture.m:87-116; super: gqmap_gpuSuper_mix_entropy.m:87-122).
+// (m, n) 0-based node; single-scale reads pixel (m, n), super the 4x4 block.
+template <bool SUPER, typename R, typename TP, typename VP>
+GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, VP I1, int M2, int Mo, int No, R eps, R lamd,
+                        bool guard, R T, R a, R u1, R u2, R o1, R o2, R p, int m, int n)
+{
+    R s, t;
+    spectral_st(p, s, t);
+    const R sq2 = R(GQ_M_SQRT2);
+    const R ax = sq2 * o1 * s, bx = sq2 * o1 * t;  // x1 = ax XI + bx XJ + u1
+    const R ay = sq2 * o2 * t, by = sq2 * o2 * s;  // x2 = ay XI + by XJ + u2
+    Sums<R> S;
+    if (!SUPER) {
+        const R I = I1[m + (int64_t)Mo * n];
+        for (int k = 0; k < K2; ++k) {
+            const R x1 = fma(ax, tab[k], fma(bx, tab[TAB_STRIDE + k], u1));
+            const R x2 = fma(ay, tab[k], fma(by, tab[TAB_STRIDE + k], u2));
+            const R d = I - sample(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
+            S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+        }
+    } else {
+        // super = sum_{i=top..bottom} sum_{j=left..right} node_pot(x1,x2,i,j): j fastest
+        R I[16];
+        const int i0 = 4 * m, j0 = 4 * n;  // 0-based top-left pixel of the block
+        for (int q = 0; q < 16; ++q) I[q] = I1[(i0 + (q >> 2)) + (int64_t)Mo * (j0 + (q & 3))];
+        for (int k = 0; k < K2; ++k) {
+            const R x1 = fma(ax, tab[k], fma(bx, tab[TAB_STRIDE + k], u1));
+            const R x2 = fma(ay, tab[k], fma(by, tab[TAB_STRIDE + k], u2));
+            R f = 0;
+            for (int q = 0; q < 16; ++q) {
+                const R d = I[q] - sample(VV, M2, Mo, No, i0 + (q >> 2) + 1, j0 + (q & 3) + 1, x1, x2);
+                f = f + GQ_SQRT(fma(d, d, eps));
+            }
+            S.add(tab, k, f);
+        }
+    }
+    return epilogue(S, -lamd, a, o1, o2, p, s, t, R(-3) * T, !guard || a != R(0));
+}
+
+}  // namespace gq

@@ -14,6 +14,12 @@
 
 #include "gqmap_internal.h"
 
+#pragma clang fp contract(off)
+#define GQ_HD __device__ __forceinline__
+#define GQ_SQRT(x) sqrt(x)
+#define GQ_UNROLL2
+#include "gqmap_math.h"
+
 namespace gq {
 
 constexpr int PROJ_NMAX = 64;
@@ -50,7 +56,7 @@ struct Mix {
         double v = 0;
         for (int l = 0; l < L; ++l) {
             const double z = (x - u[l]) / o[l];
-            v += a[l] * (exp(-0.5 * z * z) / (2.5066282746310002 * o[l]));  // normpdf
+            v += a[l] * (gq_exp(-0.5 * z * z) / (2.5066282746310002 * o[l]));  // normpdf
         }
         return -v;
     }

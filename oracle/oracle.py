@@ -1,4 +1,5 @@
-"""ctypes front-end for the C oracle (oracle/gqmap_oracle.c).
+"""ctypes front-end for the oracle library (oracle/gqmap_oracle.c literal
+restatement + oracle/gqmap_emul.cpp CPU model of the kernel arithmetic).
 
 TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
 cpu_baseline leg of bench.py -- never by the product package.  The oracle is
@@ -39,8 +40,9 @@ class OrcState(C.Structure):
 
 def build() -> str:
     path = os.path.join(_HERE, "liboracle.so")
-    src = os.path.join(_HERE, "gqmap_oracle.c")
-    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("gqmap_oracle.c", "gqmap_oracle.h", "gqmap_emul.cpp")]
+    srcs.append(os.path.join(os.path.dirname(_HERE), "gqmap-opticalflow_amd", "csrc", "gqmap_math.h"))
+    if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return path
 
@@ -201,4 +203,37 @@ def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0) -> np.ndarray:
     out = np.zeros((M, N, 2), order="F")
     lib().orc_get_map(_p(alpha), _p(muu), _p(sigu), _p(muv), _p(sigv), M, N, L, _p(out),
                       nthreads)
+    return out
+
+
+def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
+            T: float | None = None, nthreads: int = 0, fp32: bool = False):
+    """CPU model of the HIP kernel (oracle/gqmap_emul.cpp): bit-identical to
+    libgqmap.so for the same quadrature nodes X, W (pass the product's
+    gauss_hermite(K)).  Returns (done, trace[done,3], T)."""
+    I1 = _f64(I1)
+    Mo, No = I1.shape
+    p = make_params(opts, Mo, No)
+    VV = get_vv(I2)
+    X, W = _f64(np.asarray(X, dtype=np.float64)), _f64(np.asarray(W, dtype=np.float64))
+    Tbox = (C.c_double * 1)(p.T if T is None else T)
+    trace = np.zeros((max(n_iter, 1), 3))
+    cs = state.cstruct()
+    f = lib().emu_run
+    f.restype = C.c_int
+    done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
+             _p(trace), nthreads, int(fp32))
+    if done < 0:
+        raise RuntimeError("emu_run failed")
+    return done, trace[:done].copy(), Tbox[0]
+
+
+def emu_math(fn: int, x) -> np.ndarray:
+    """Host evaluation of the shared deterministic math (0 sqrt, 1 log, 2 exp)."""
+    x = _f64(np.asarray(x, dtype=np.float64).ravel())
+    out = np.zeros_like(x)
+    f = lib().emu_math
+    f.restype = None
+    f.argtypes = [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int64]
+    f(fn, _p(x), _p(out), x.size)
     return out
