@@ -1,0 +1,27 @@
+"""Profiling driver: C2 (RubberWhale 388x584, mixture, L=1, K=9) iterations,
+no torch.  Usage: python scripts/prof_iter.py [its] [fp64|fp32] [mixture|super]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import setup_problem  # noqa: E402
+from gqmap_opticalflow_amd import Engine  # noqa: E402
+
+its = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+prec = sys.argv[2] if len(sys.argv) > 2 else "fp64"
+engine = sys.argv[3] if len(sys.argv) > 3 else "mixture"
+if engine == "super":
+    I1, I2, flo, unk, o = setup_problem("Urban3", 3, 11)
+    o.update(temperature=0.2, drate=0.75, lambdas=16.0)
+else:
+    I1, I2, flo, unk, o = setup_problem("rubberwhale", 1, 9)
+with Engine(o, I1, I2, engine, prec) as eng:
+    eng.init_state(0)
+    done, tot, ker = eng.run_timed(its)
+    t = time.perf_counter()
+    eng.run(its)
+    eng.synchronize()
+    dt = time.perf_counter() - t
+print(f"{engine} {prec}: {done} its, events total {tot:.3f} ms, k_iter sum {ker:.3f} ms "
+      f"({ker / its * 1e3:.1f} us/it); graph run {dt / its * 1e6:.1f} us/it")
