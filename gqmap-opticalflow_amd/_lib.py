@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libgqmap.so")
+LIB_PATH = os.environ.get("GQMAP_LIB", os.path.join(PKG_DIR, "libgqmap.so"))
 
 GQMAP_OK = 0
 ENGINE_MIXTURE, ENGINE_SUPER = 0, 1

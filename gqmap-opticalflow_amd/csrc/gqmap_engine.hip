@@ -57,7 +57,19 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 
 #define GQ_HD __device__ __forceinline__
 #define GQ_SQRT(x) gq::gq_sqrt_dev(x)
-#define GQ_UNROLL2 _Pragma("unroll 2")
+#ifndef GQ_EDGE_UNROLL_N
+#define GQ_EDGE_UNROLL_N 2
+#endif
+#ifndef GQ_NODE_UNROLL_N
+#define GQ_NODE_UNROLL_N 1
+#endif
+#ifndef GQ_MIN_WAVES
+#define GQ_MIN_WAVES 1
+#endif
+#define GQ_STR2(x) #x
+#define GQ_PRAGMA_UNROLL(n) _Pragma(GQ_STR2(unroll n))
+#define GQ_UNROLL2 GQ_PRAGMA_UNROLL(GQ_EDGE_UNROLL_N)
+#define GQ_NODE_UNROLL GQ_PRAGMA_UNROLL(GQ_NODE_UNROLL_N)
 #include "gqmap_math.h"
 
 namespace gq {
@@ -129,7 +141,7 @@ __device__ __forceinline__ bool finite_d(double x) { return (bits_of(x) & 0x7ff0
 // fused iteration kernel
 // ---------------------------------------------------------------------------
 template <typename R, bool SUPER>
-__global__ __launch_bounds__(BLOCK) void k_iter(IterParams<R> P)
+__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R> P)
 {
     const Ctl *ctl = P.ctl;
     if (ctl->stop) return;

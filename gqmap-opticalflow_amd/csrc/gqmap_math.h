@@ -14,8 +14,8 @@
 //     not depend on the order in which tiles, waves or threads add them.
 //
 // The includer defines GQ_HD (e.g. `__device__ __forceinline__` or `inline`),
-// GQ_SQRT(x) for double and float and GQ_UNROLL2 (a loop-unroll pragma or
-// nothing), makes fma/fmin/fmax/floorf/fminf/fmaxf visible for float and double, then includes
+// GQ_SQRT(x) for double and float, GQ_UNROLL2 and GQ_NODE_UNROLL (loop-unroll
+// pragmas or nothing), makes fma/fmin/fmax/floorf/fminf/fmaxf visible for float and double, then includes
 // this file.
 //
 // Reference lines this arithmetic restates: node_pot / edge_pot
@@ -308,6 +308,7 @@ GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, VP I1, int M2, int Mo, int No, R 
     Sums<R> S;
     if (!SUPER) {
         const R I = I1[m + (int64_t)Mo * n];
+        GQ_NODE_UNROLL
         for (int k = 0; k < K2; ++k) {
             const R x1 = fma(ax, tab[k], fma(bx, tab[TAB_STRIDE + k], u1));
             const R x2 = fma(ay, tab[k], fma(by, tab[TAB_STRIDE + k], u2));

@@ -18,6 +18,7 @@
 #define GQ_HD __device__ __forceinline__
 #define GQ_SQRT(x) sqrt(x)
 #define GQ_UNROLL2
+#define GQ_NODE_UNROLL
 #include "gqmap_math.h"
 
 namespace gq {

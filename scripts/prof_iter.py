@@ -20,8 +20,9 @@ with Engine(o, I1, I2, engine, prec) as eng:
     eng.init_state(0)
     done, tot, ker = eng.run_timed(its)
     t = time.perf_counter()
-    eng.run(its)
+    _, tr = eng.run(its)
     eng.synchronize()
     dt = time.perf_counter() - t
+    chk = f"{tr[-1, 0]:.17g}"
 print(f"{engine} {prec}: {done} its, events total {tot:.3f} ms, k_iter sum {ker:.3f} ms "
-      f"({ker / its * 1e3:.1f} us/it); graph run {dt / its * 1e6:.1f} us/it")
+      f"({ker / its * 1e3:.1f} us/it); graph run {dt / its * 1e6:.1f} us/it chk={chk}")
