@@ -190,7 +190,11 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R> P)
 #pragma unroll
         for (int q = 0; q < NPLANES; ++q) own[q] = valid ? src[i + MNL * q] : R(0);
         Grad<R> nd{};
+#ifndef GQ_ABL_NONODE
         if (inner)
+#else
+        if (inner && own[0] == R(12345.678))  // timing ablation only
+#endif
             nd = node_grad<SUPER, R>(tab, P.K2, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, P.lamd,
                                      P.guard != 0, T, a, own[0], own[1], own[2], own[3], own[4], m, n);
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
@@ -220,7 +224,11 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R> P)
             const bool r_inner = rm < M && rn < N && interior(rm, rn);
             const bool need = own_edge ? (inner || (valid && r_inner)) : (hm >= 0 && hn >= 0 && r_inner);
             Grad<R> g{};
+#ifdef GQ_ABL_NOEDGE
+            if (need && a == R(12345.678)) {  // timing ablation only
+#else
             if (need) {
+#endif
                 const int64_t h = hm + (int64_t)M * hn + MN * l;
                 const int64_t r = rm + (int64_t)M * rn + MN * l;
                 const R u1 = own_edge ? (uv ? own[1] : own[0]) : src[h + MNL * uv];
