@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -906,7 +907,8 @@ gqmap_status gqmap_run(gqmap_ctx *c, int n_iter, int *n_done, double *trace)
         // the device trace ring holds TRACE_CAP iterations: drain it per chunk
         const int chunk = std::min(n_iter - total, TRACE_CAP);
         int left = chunk;
-        if (left >= GRAPH_CHUNK) {
+        static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
+        if (left >= GRAPH_CHUNK && !no_graph) {
             if ((s = ensure_graph(c)) != GQMAP_OK) return s;
             while (left >= GRAPH_CHUNK) {
                 GQ_HIP(hipGraphLaunch(c->graph, c->stream));

@@ -164,9 +164,9 @@ GQ_HD R bicubic_cell(VP c, int M2, R so, R to)
     keys4(to, t0, t1, t2, t3);
     keys4(so, s0, s1, s2, s3);
 #ifdef GQ_ABL_NOGATHER  // timing ablation only: no memory traffic for the taps
-    const R v0 = t0 + s1, v1 = t1 * s2, v2 = t2 - s3, v3 = t3 + s0;
-    return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0))) * R(0.25) + (R)(int64_t)(c - (VP)0) * R(1e-30);
-#endif
+    const R a0 = t0 + s1, a1 = t1 * s2, a2 = t2 - s3, a3 = t3 + s0;
+    return fma(s3, a3, fma(s2, a2, fma(s1, a1, s0 * a0))) * R(0.25) + (R)(int64_t)(c - (VP)0) * R(1e-30);
+#else
     const R v0 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
     c += M2;
     const R v1 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
@@ -175,6 +175,7 @@ GQ_HD R bicubic_cell(VP c, int M2, R so, R to)
     c += M2;
     const R v3 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
     return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0))) * R(0.25);
+#endif
 }
 
 // interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV.
