@@ -94,9 +94,9 @@ struct Ctl {
     double w[GQMAP_LMAX];
 };
 
-template <typename R>
+template <typename R, typename VT = R>
 struct IterParams {
-    const R *__restrict__ VV;   // (Mo+2) x (No+2) cubic-convolution padded I2
+    const VT *__restrict__ VV;  // (Mo+2) x (No+2) cubic-convolution padded I2 (VT: storage type)
     const R *__restrict__ I1;   // Mo x No
     R *st0;
     R *st1;
@@ -141,8 +141,8 @@ __device__ __forceinline__ bool finite_d(double x) { return (bits_of(x) & 0x7ff0
 // ---------------------------------------------------------------------------
 // fused iteration kernel
 // ---------------------------------------------------------------------------
-template <typename R, bool SUPER>
-__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R> P)
+template <typename R, typename VT, bool SUPER>
+__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> P)
 {
     const Ctl *ctl = P.ctl;
     if (ctl->stop) return;
@@ -419,8 +419,8 @@ __device__ __forceinline__ double wave_sum(double v)
 }
 
 // profile_logP (gqmap_gpu_mixture.m:148-154; super :152-169): per-block partials.
-template <typename R, bool SUPER>
-__global__ __launch_bounds__(256) void k_logp(IterParams<R> P, const R *__restrict__ map,
+template <typename R, typename VT, bool SUPER>
+__global__ __launch_bounds__(256) void k_logp(IterParams<R, VT> P, const R *__restrict__ map,
                                               double *partials)
 {
     const int64_t MN = (int64_t)P.M * P.N;
@@ -494,6 +494,7 @@ struct gqmap_ctx {
     double *d_trace = nullptr;
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     bool have_images = false, have_state = false;
+    bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
     hipGraphExec_t graph = nullptr;
     double tab_host[NTAB * TS];
 };
@@ -517,12 +518,12 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     return GQMAP_OK;
 }
 
-template <typename R>
-IterParams<R> iter_params(const gqmap_ctx *c)
+template <typename R, typename VT>
+IterParams<R, VT> iter_params(const gqmap_ctx *c)
 {
-    IterParams<R> P;
+    IterParams<R, VT> P;
     const gqmap_options &o = c->opt;
-    P.VV = (const R *)c->d_VV;
+    P.VV = (const VT *)c->d_VV;
     P.I1 = (const R *)c->d_I1;
     P.st0 = (R *)c->d_st[0];
     P.st1 = (R *)c->d_st[1];
@@ -557,20 +558,23 @@ FinParams fin_params(const gqmap_ctx *c)
     return F;
 }
 
-template <typename R, bool SUPER>
+template <typename R, typename VT, bool SUPER>
 void launch_iter_t(gqmap_ctx *c)
 {
-    k_iter<R, SUPER><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R>(c));
+    k_iter<R, VT, SUPER><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
 }
 
 void launch_iter(gqmap_ctx *c)
 {
     if (c->fp32) {
-        if (c->super_) launch_iter_t<float, true>(c);
-        else launch_iter_t<float, false>(c);
+        if (c->super_) launch_iter_t<float, float, true>(c);
+        else launch_iter_t<float, float, false>(c);
+    } else if (c->vv32) {
+        if (c->super_) launch_iter_t<double, float, true>(c);
+        else launch_iter_t<double, float, false>(c);
     } else {
-        if (c->super_) launch_iter_t<double, true>(c);
-        else launch_iter_t<double, false>(c);
+        if (c->super_) launch_iter_t<double, double, true>(c);
+        else launch_iter_t<double, double, false>(c);
     }
 }
 
@@ -770,7 +774,7 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
         GQ_CHECK(Mo % 4 == 0 && No % 4 == 0, GQMAP_ERR_INVALID_ARG,
                  "super engine needs Mo,No divisible by 4 (got %dx%d)", Mo, No);
     DeviceGuard dg(c->device);
-    const bool resize = Mo != c->Mo || No != c->No;
+    bool resize = Mo != c->Mo || No != c->No;
     c->Mo = Mo;
     c->No = No;
     c->M = c->super_ ? Mo / 4 : Mo;
@@ -780,19 +784,36 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
     c->MNL = (int64_t)c->M * c->N * c->L;
     std::vector<double> VV((size_t)(Mo + 2) * (No + 2));
     build_padded(I2, Mo, No, VV.data());
+    // fp64 engine: keep the padded image in float when that is exact (frames
+    // from rgb2gray are integers; their cubic padding stays in [-510, 765]):
+    // same values, half the gather bytes.
+    bool vv32 = c->fp32;
+    if (!vv32 && !std::getenv("GQMAP_VV64")) {
+        vv32 = true;
+        for (double v : VV)
+            if ((double)(float)v != v) { vv32 = false; break; }
+    }
+    if (vv32 != c->vv32) resize = true;
+    c->vv32 = vv32;
+    const size_t vsz = vv32 ? sizeof(float) : sizeof(double);
     if (resize || !c->d_VV) {
         drop_graph(c);
         if (c->d_VV) (void)hipFree(c->d_VV);
         if (c->d_I1) (void)hipFree(c->d_I1);
         c->d_VV = c->d_I1 = nullptr;
-        GQ_HIP(hipMalloc(&c->d_VV, VV.size() * c->rsz));
+        GQ_HIP(hipMalloc(&c->d_VV, VV.size() * vsz));
         GQ_HIP(hipMalloc(&c->d_I1, (size_t)Mo * No * c->rsz));
         gqmap_status s = alloc_grid(c);
         if (s != GQMAP_OK) return s;
         c->have_state = false;
     }
     gqmap_status s;
-    if ((s = upload(c, c->d_VV, VV.data(), VV.size())) != GQMAP_OK) return s;
+    if (vv32) {
+        std::vector<float> v32(VV.begin(), VV.end());
+        GQ_HIP(hipMemcpy(c->d_VV, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice));
+    } else if ((s = upload(c, c->d_VV, VV.data(), VV.size())) != GQMAP_OK) {
+        return s;
+    }
     if ((s = upload(c, c->d_I1, I1, (size_t)Mo * No)) != GQMAP_OK) return s;
     c->have_images = true;
     return GQMAP_OK;
@@ -1032,11 +1053,14 @@ gqmap_status gqmap_log_p(gqmap_ctx *c, const double *map, double *logp)
     gqmap_status s = upload(c, d_map, map, 2 * MN);
     if (s == GQMAP_OK) {
         if (c->fp32) {
-            if (c->super_) k_logp<float, true><<<blocks, 256, 0, c->stream>>>(iter_params<float>(c), (const float *)d_map, d_part);
-            else k_logp<float, false><<<blocks, 256, 0, c->stream>>>(iter_params<float>(c), (const float *)d_map, d_part);
+            if (c->super_) k_logp<float, float, true><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
+            else k_logp<float, float, false><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
+        } else if (c->vv32) {
+            if (c->super_) k_logp<double, float, true><<<blocks, 256, 0, c->stream>>>(iter_params<double, float>(c), (const double *)d_map, d_part);
+            else k_logp<double, float, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, float>(c), (const double *)d_map, d_part);
         } else {
-            if (c->super_) k_logp<double, true><<<blocks, 256, 0, c->stream>>>(iter_params<double>(c), (const double *)d_map, d_part);
-            else k_logp<double, false><<<blocks, 256, 0, c->stream>>>(iter_params<double>(c), (const double *)d_map, d_part);
+            if (c->super_) k_logp<double, double, true><<<blocks, 256, 0, c->stream>>>(iter_params<double, double>(c), (const double *)d_map, d_part);
+            else k_logp<double, double, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, double>(c), (const double *)d_map, d_part);
         }
         std::vector<double> part(blocks);
         hipError_t e = hipGetLastError();

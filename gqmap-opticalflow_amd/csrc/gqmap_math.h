@@ -301,8 +301,8 @@ GQ_HD Grad<R> edge_grad(TP tab, int K2, R eps, R lams, bool guard, R T, R a, R u
 
 // node_grad_spectral (gqmap_gpu_mixture.m:87-116; super: gqmap_gpuSuper_mix_entropy.m:87-122).
 // (m, n) 0-based node; single-scale reads pixel (m, n), super the 4x4 block.
-template <bool SUPER, typename R, typename TP, typename VP>
-GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, VP I1, int M2, int Mo, int No, R eps, R lamd,
+template <bool SUPER, typename R, typename TP, typename VP, typename IP>
+GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R eps, R lamd,
                         bool guard, R T, R a, R u1, R u2, R o1, R o2, R p, int m, int n)
 {
     R s, t;
