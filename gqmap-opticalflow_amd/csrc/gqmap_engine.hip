@@ -178,7 +178,6 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     // in_up[uv][q][ln*16+lm]: du2/do2 of the edge from (m-1,n); in_left: from (m,n-1)
     __shared__ R in_up[2][2][BLOCK];
     __shared__ R in_left[2][2][BLOCK];
-    __shared__ R nd_sh[7][BLOCK];
     __shared__ fix128 red[GQMAP_LMAX + NFIX][4];
 
     fix128 fE = 0, fmu = 0, fsg = 0;
@@ -188,26 +187,21 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     for (int l = 0; l < P.L; ++l) {
         const R a = R(ctl->alpha[l]);
         const int64_t i = m + (int64_t)M * n + MN * l;
-        // ---- phase 1: node term; only its 7 results stay (in LDS) ------------
-        {
-            Grad<R> nd{};
+        R own[NPLANES];
+#pragma unroll
+        for (int q = 0; q < NPLANES; ++q) own[q] = valid ? src[i + MNL * q] : R(0);
+        Grad<R> nd{};
 #ifndef GQ_ABL_NONODE
-            if (inner)
+        if (inner)
 #else
-            if (inner && a == R(12345.678))  // timing ablation only
+        if (inner && own[0] == R(12345.678))  // timing ablation only
 #endif
-                nd = node_grad<SUPER, R>(tab, P.K2, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, P.lamd,
-                                         P.guard != 0, T, a, src[i], src[i + MNL], src[i + 2 * MNL],
-                                         src[i + 3 * MNL], src[i + 4 * MNL], m, n);
-            nd_sh[0][tid] = nd.du1; nd_sh[1][tid] = nd.du2; nd_sh[2][tid] = nd.do1;
-            nd_sh[3][tid] = nd.do2; nd_sh[4][tid] = nd.dp;
-            nd_sh[5][tid] = nd.E; nd_sh[6][tid] = nd.da;
-        }
-        // ---- phase 2: edge jobs e = dir + 2*uv (rou plane 5+e) for the owned
-        // down/right edges, then job 4: wave 0 recomputes the 64 halo edges
-        // entering the tile from the row above / the column to the left.  One
-        // edge body whose inputs are re-read (L1 hits), streamed into a few
-        // accumulators and LDS.
+            nd = node_grad<SUPER, R>(tab, P.K2, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, P.lamd,
+                                     P.guard != 0, T, a, own[0], own[1], own[2], own[3], own[4], m, n);
+        // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
+        // edges, then job 4: wave 0 recomputes the 64 halo edges entering
+        // the tile from the row above / the column to the left.  One edge
+        // body, streamed into accumulators and LDS, keeps VGPRs low.
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
         R eE = 0, eda = 0;                                     // sum over the 4 edges
@@ -238,9 +232,12 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
 #endif
                 const int64_t h = hm + (int64_t)M * hn + MN * l;
                 const int64_t r = rm + (int64_t)M * rn + MN * l;
-                g = edge_grad<R>(tab, P.K2, P.epsn, P.lams, P.guard != 0, T, a, src[h + MNL * uv],
-                                 src[r + MNL * uv], src[h + MNL * (2 + uv)], src[r + MNL * (2 + uv)],
-                                 src[h + MNL * (5 + dir + 2 * uv)]);
+                const R u1 = own_edge ? (uv ? own[1] : own[0]) : src[h + MNL * uv];
+                const R o1 = own_edge ? (uv ? own[3] : own[2]) : src[h + MNL * (2 + uv)];
+                const R p = own_edge ? (e == 0 ? own[5] : e == 1 ? own[6] : e == 2 ? own[7] : own[8])
+                                     : src[h + MNL * (5 + dir + 2 * uv)];
+                g = edge_grad<R>(tab, P.K2, P.epsn, P.lams, P.guard != 0, T, a, u1,
+                                 src[r + MNL * uv], o1, src[r + MNL * (2 + uv)], p);
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
@@ -259,26 +256,25 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
             }
         }
         __syncthreads();
-        // ---- phase 3: gradient assembly, clamped ascent, exact sums -----------
         fix128 fda = 0;
         if (inner) {
             // dmuu = dmuu + sum(dmu1(:,:,:,:,1),4) + circshift(dmu2(..1,1),1) + circshift(dmu2(..2,1),1,2)
-            const R gmu_u = ((nd_sh[0][tid] + sum_mu0) + in_up[0][0][tid]) + in_left[0][0][tid];
-            const R gmu_v = ((nd_sh[1][tid] + sum_mu1) + in_up[1][0][tid]) + in_left[1][0][tid];
-            const R gsg_u = ((nd_sh[2][tid] + sum_sg0) + in_up[0][1][tid]) + in_left[0][1][tid];
-            const R gsg_v = ((nd_sh[3][tid] + sum_sg1) + in_up[1][1][tid]) + in_left[1][1][tid];
+            const R gmu_u = ((nd.du1 + sum_mu0) + in_up[0][0][tid]) + in_left[0][0][tid];
+            const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][tid]) + in_left[1][0][tid];
+            const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][tid]) + in_left[0][1][tid];
+            const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][tid]) + in_left[1][1][tid];
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
-            dst[i + MNL * 0] = cl(src[i] + gmu_u * step, P.minu, P.maxu);
-            dst[i + MNL * 1] = cl(src[i + MNL] + gmu_v * step, P.minv, P.maxv);
-            dst[i + MNL * 2] = cl(src[i + 2 * MNL] + gsg_u * step, P.sig_lo, P.sig_hi);
-            dst[i + MNL * 3] = cl(src[i + 3 * MNL] + gsg_v * step, P.sig_lo, P.sig_hi);
-            dst[i + MNL * 4] = cl(src[i + 4 * MNL] + nd_sh[4][tid] * step, -P.corr, P.corr);
-            dst[i + MNL * 5] = cl(src[i + 5 * MNL] + drou0 * step, -P.corr, P.corr);
-            dst[i + MNL * 6] = cl(src[i + 6 * MNL] + drou1 * step, -P.corr, P.corr);
-            dst[i + MNL * 7] = cl(src[i + 7 * MNL] + drou2 * step, -P.corr, P.corr);
-            dst[i + MNL * 8] = cl(src[i + 8 * MNL] + drou3 * step, -P.corr, P.corr);
+            dst[i + MNL * 0] = cl(own[0] + gmu_u * step, P.minu, P.maxu);
+            dst[i + MNL * 1] = cl(own[1] + gmu_v * step, P.minv, P.maxv);
+            dst[i + MNL * 2] = cl(own[2] + gsg_u * step, P.sig_lo, P.sig_hi);
+            dst[i + MNL * 3] = cl(own[3] + gsg_v * step, P.sig_lo, P.sig_hi);
+            dst[i + MNL * 4] = cl(own[4] + nd.dp * step, -P.corr, P.corr);
+            dst[i + MNL * 5] = cl(own[5] + drou0 * step, -P.corr, P.corr);
+            dst[i + MNL * 6] = cl(own[6] + drou1 * step, -P.corr, P.corr);
+            dst[i + MNL * 7] = cl(own[7] + drou2 * step, -P.corr, P.corr);
+            dst[i + MNL * 8] = cl(own[8] + drou3 * step, -P.corr, P.corr);
             // per-node contributions to the global sums (exact fixed point)
-            const double cE = (double)nd_sh[5][tid] + (double)eE, cda = (double)nd_sh[6][tid] + (double)eda;
+            const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
             const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
             nonfinite += !finite_d(cE) + !finite_d(cda) + !finite_d(cmu) + !finite_d(csg);
             fE += to_fix(cE);
