@@ -71,6 +71,7 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #define GQ_PRAGMA_UNROLL(n) _Pragma(GQ_STR2(unroll n))
 #define GQ_UNROLL2 GQ_PRAGMA_UNROLL(GQ_EDGE_UNROLL_N)
 #define GQ_NODE_UNROLL GQ_PRAGMA_UNROLL(GQ_NODE_UNROLL_N)
+#define GQ_UNROLL_FULL _Pragma("unroll")
 #include "gqmap_math.h"
 
 namespace gq {

@@ -14,8 +14,8 @@
 //     not depend on the order in which tiles, waves or threads add them.
 //
 // The includer defines GQ_HD (e.g. `__device__ __forceinline__` or `inline`),
-// GQ_SQRT(x) for double and float, GQ_UNROLL2 and GQ_NODE_UNROLL (loop-unroll
-// pragmas or nothing), makes fma/fmin/fmax/floorf/fminf/fmaxf visible for float and double, then includes
+// GQ_SQRT(x) for double and float, GQ_UNROLL2, GQ_NODE_UNROLL and GQ_UNROLL_FULL
+// (loop-unroll pragmas or nothing), makes fma/fmin/fmax/floorf/fminf/fmaxf visible for float and double, then includes
 // this file.
 //
 // Reference lines this arithmetic restates: node_pot / edge_pot
@@ -210,6 +210,63 @@ GQ_HD float sample(VP VV, int M2, int Mo, int No, int ii, int jj, float x1, floa
 }
 
 // ---------------------------------------------------------------------------
+// 4x4 super-pixel data term (gqmap_gpuSuper_mix_entropy.m:94-105):
+//   sum_{i=top..bottom} sum_{j=left..right} sqrt(eps + (I1(i,j) - interp(j+x1, i+x2))^2)
+// When no sample of the block is clamped (left+x1 >= 1, right+x1 <= No-1 and
+// the same for rows) every sample has the fractional offset
+// (so, to) = (x1 - floor(x1), x2 - floor(x2)) and pixel (i,j) interpolates the
+// cell (i + floor(x2), j + floor(x1)): the 16 cells tile one 7x7 tap window,
+// so the 28 column sums are shared (49 taps instead of 256).  Each output
+// uses exactly the fma sequence of bicubic_cell.  Blocks touching the border
+// take the reference per-sample position arithmetic (sample()).
+// I[q], q = 4*di + dj (j fastest, the reference loop order).
+// ---------------------------------------------------------------------------
+template <typename R, typename VP>
+GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x2, R eps,
+                        const R (&I)[16])
+{
+    const bool safe = R(j0 + 1) + x1 >= R(1) && R(j0 + 4) + x1 <= R(No - 1) &&
+                      R(i0 + 1) + x2 >= R(1) && R(i0 + 4) + x2 <= R(Mo - 1);
+    R f = 0;
+    if (safe) {
+        const R fx = floor(x1), fy = floor(x2);
+        const R so = x1 - fx, to = x2 - fy;
+        R t0, t1, t2, t3, s0, s1, s2, s3;
+        keys4(to, t0, t1, t2, t3);
+        keys4(so, s0, s1, s2, s3);
+        // window origin: padded row i0 + fy, padded column j0 + fx (0-based)
+        VP c = VV + (i0 + (int)fy) + (int64_t)M2 * (j0 + (int)fx);
+        R out[4][4];
+        GQ_UNROLL_FULL
+        for (int a = 0; a < 7; ++a, c += M2) {
+            R v[4];
+            GQ_UNROLL_FULL
+            for (int di = 0; di < 4; ++di)
+                v[di] = fma(c[di + 3], t3, fma(c[di + 2], t2, fma(c[di + 1], t1, c[di] * t0)));
+            GQ_UNROLL_FULL
+            for (int dj = 0; dj < 4; ++dj) {
+                const int k = a - dj;  // this column is tap k of output column dj
+                if (k < 0 || k > 3) continue;
+                const R sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+                GQ_UNROLL_FULL
+                for (int di = 0; di < 4; ++di)
+                    out[di][dj] = k == 0 ? sk * v[di] : fma(sk, v[di], out[di][dj]);
+            }
+        }
+        for (int q = 0; q < 16; ++q) {
+            const R d = I[q] - out[q >> 2][q & 3] * R(0.25);
+            f = f + GQ_SQRT(fma(d, d, eps));
+        }
+    } else {
+        for (int q = 0; q < 16; ++q) {
+            const R d = I[q] - sample(VV, M2, Mo, No, i0 + (q >> 2) + 1, j0 + (q & 3) + 1, x1, x2);
+            f = f + GQ_SQRT(fma(d, d, eps));
+        }
+    }
+    return f;
+}
+
+// ---------------------------------------------------------------------------
 // spectral quadrature of the node / edge potentials
 // ---------------------------------------------------------------------------
 template <typename R>
@@ -328,12 +385,7 @@ GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R 
         for (int k = 0; k < K2; ++k) {
             const R x1 = fma(ax, tab[k], fma(bx, tab[TAB_STRIDE + k], u1));
             const R x2 = fma(ay, tab[k], fma(by, tab[TAB_STRIDE + k], u2));
-            R f = 0;
-            for (int q = 0; q < 16; ++q) {
-                const R d = I[q] - sample(VV, M2, Mo, No, i0 + (q >> 2) + 1, j0 + (q & 3) + 1, x1, x2);
-                f = f + GQ_SQRT(fma(d, d, eps));
-            }
-            S.add(tab, k, f);
+            S.add(tab, k, super_block_sum<R>(VV, M2, Mo, No, i0, j0, x1, x2, eps, I));
         }
     }
     return epilogue(S, -lamd, a, o1, o2, p, s, t, R(-3) * T, !guard || a != R(0));
