@@ -41,7 +41,7 @@ class GqmapOptions(C.Structure):
         ("guard_a", C.c_int), ("t_decay_every", C.c_int), ("t_min", C.c_double),
         ("step0", C.c_double), ("step_decay", C.c_double),
         ("sig_lo", C.c_double), ("sig_hi", C.c_double), ("corr_tor", C.c_double),
-        ("tor", C.c_double),
+        ("tor", C.c_double), ("split", C.c_int),
     ]
 
 
@@ -56,7 +56,7 @@ class GqmapState(C.Structure):
 class GqmapInfo(C.Structure):
     _fields_ = [("Mo", C.c_int), ("No", C.c_int), ("M", C.c_int), ("N", C.c_int),
                 ("L", C.c_int), ("K", C.c_int), ("it", C.c_int), ("stopped", C.c_int),
-                ("T", C.c_double), ("device", C.c_int)]
+                ("T", C.c_double), ("device", C.c_int), ("split", C.c_int)]
 
 
 class GqmapError(RuntimeError):

@@ -139,12 +139,42 @@ __device__ __forceinline__ fix128 wave_sum_fix(fix128 v)
 }
 __device__ __forceinline__ bool finite_d(double x) { return (bits_of(x) & 0x7ff0000000000000ULL) != 0x7ff0000000000000ULL; }
 
+__device__ __forceinline__ double shfl_xor_r(double v, int o) { return __shfl_xor(v, o, 64); }
+__device__ __forceinline__ float shfl_xor_r(float v, int o) { return __shfl_xor(v, o, 64); }
+
+// Combine the Q partial quadrature sums of a node's lane group (adjacent
+// lanes): the xor butterfly of gqmap_math.h's butterfly(), every lane ends
+// with the same total.
+template <int Q, typename R>
+__device__ __forceinline__ Sums<R> lane_combine(Sums<R> S)
+{
+#pragma unroll
+    for (int o = Q / 2; o > 0; o >>= 1) {
+        S.s0 = S.s0 + shfl_xor_r(S.s0, o);
+        S.sxi = S.sxi + shfl_xor_r(S.sxi, o);
+        S.sxj = S.sxj + shfl_xor_r(S.sxj, o);
+        S.sa = S.sa + shfl_xor_r(S.sa, o);
+        S.sm = S.sm + shfl_xor_r(S.sm, o);
+        S.sx = S.sx + shfl_xor_r(S.sx, o);
+    }
+    return S;
+}
+
 // ---------------------------------------------------------------------------
 // fused iteration kernel
+//
+// A workgroup owns a TM x TM tile of nodes; each node is served by Q adjacent
+// lanes (Q = 1 for full-resolution grids; 4 or 16 for the small node grids of
+// the super engine and coarse pyramid levels, so they still fill 256 CUs).
+// Lane j of a node sums the quadrature points k = j, j+Q, ... and the lanes
+// combine with an xor butterfly (the spec's butterfly()).
 // ---------------------------------------------------------------------------
-template <typename R, typename VT, bool SUPER>
+template <typename R, typename VT, bool SUPER, int Q>
 __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> P)
 {
+    constexpr int TPIX = BLOCK / Q;                   // nodes per tile
+    constexpr int TM = Q == 1 ? 16 : Q == 4 ? 8 : 4;  // tile side
+    static_assert(TM * TM == TPIX, "tile");
     const Ctl *ctl = P.ctl;
     if (ctl->stop) return;
     const int it = ctl->it;
@@ -166,24 +196,30 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     }
     const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
     const int tid = threadIdx.x;
-    const int lm = tid & (TILE - 1), ln = tid >> 4;
-    const int m0 = tm * TILE, n0 = tn * TILE;
+    const int pix = tid / Q, kj = tid % Q;  // node within the tile, lane within the node
+    const int lm = pix % TM, ln = pix / TM;
+    const int m0 = tm * TM, n0 = tn * TM;
     const int m = m0 + lm, n = n0 + ln;
     const int M = P.M, N = P.N;
     const int64_t MNL = P.MNL, MN = (int64_t)M * N;
     const bool valid = m < M && n < N;
     auto interior = [&](int mm, int nn) { return mm >= 1 && mm <= M - 2 && nn >= 1 && nn <= N - 2; };
     const bool inner = valid && interior(m, n);
+    const bool lead = kj == 0;  // the lane that owns the node's outputs
     const ctab_t<R> tab = as_const(P.tab);
+    const int K2 = P.K2;
 
-    // in_up[uv][q][ln*16+lm]: du2/do2 of the edge from (m-1,n); in_left: from (m,n-1)
-    __shared__ R in_up[2][2][BLOCK];
-    __shared__ R in_left[2][2][BLOCK];
+    // in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n); in_left: from (m,n-1)
+    __shared__ R in_up[2][2][TPIX];
+    __shared__ R in_left[2][2][TPIX];
     __shared__ fix128 red[GQMAP_LMAX + NFIX][4];
 
     fix128 fE = 0, fmu = 0, fsg = 0;
     int nonfinite = 0;
     const int wave = tid >> 6, lane = tid & 63;
+    // halo: 4*TM edges (top row and left column, u and v) x Q lanes, whole waves
+    constexpr int HALO_LANES = 4 * TM * Q;
+    const bool halo_lane = tid < HALO_LANES;
 
     for (int l = 0; l < P.L; ++l) {
         const R a = R(ctl->alpha[l]);
@@ -193,35 +229,40 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
         for (int q = 0; q < NPLANES; ++q) own[q] = valid ? src[i + MNL * q] : R(0);
         Grad<R> nd{};
 #ifndef GQ_ABL_NONODE
-        if (inner)
+        if (inner) {
 #else
-        if (inner && own[0] == R(12345.678))  // timing ablation only
+        if (inner && own[0] == R(12345.678)) {  // timing ablation only
 #endif
-            nd = node_grad<SUPER, R>(tab, P.K2, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, P.lamd,
-                                     P.guard != 0, T, a, own[0], own[1], own[2], own[3], own[4], m, n);
+            const NodeCoef<R> c = node_coef(own[2], own[3], own[4]);
+            Sums<R> S = node_sums<SUPER>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
+                                         own[0], own[1], m, n);
+            if (Q > 1) S = lane_combine<Q>(S);
+            nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, own[2], own[3], own[4]);
+        }
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
-        // edges, then job 4: wave 0 recomputes the 64 halo edges entering
-        // the tile from the row above / the column to the left.  One edge
-        // body, streamed into accumulators and LDS, keeps VGPRs low.
+        // edges, then job 4 on the halo lanes: the edges entering the tile from
+        // the row above / the column to the left.  One edge body, streamed into
+        // accumulators and LDS, keeps VGPRs low.
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
         R eE = 0, eda = 0;                                     // sum over the 4 edges
-        const int njobs = tid < 64 ? 5 : 4;  // wave-uniform
+        const int njobs = halo_lane ? 5 : 4;  // wave-uniform
 #pragma unroll 1
         for (int e = 0; e < njobs; ++e) {
-            int dir, uv, hm, hn, rm, rn;
+            int dir, uv, hm, hn, rm, rn, hr = 0;
             const bool own_edge = e < 4;
             if (own_edge) {
                 dir = e & 1; uv = e >> 1;
                 hm = m; hn = n;
                 rm = dir == 0 ? m + 1 : m; rn = dir == 1 ? n + 1 : n;
             } else {
-                const bool top = tid < 32;
-                uv = (tid >> 4) & 1;
-                const int r = tid & 15;
+                const int h = tid / Q;  // halo edge index
+                const bool top = h < 2 * TM;
+                uv = (h / TM) & 1;
+                hr = h % TM;
                 dir = top ? 0 : 1;
-                hm = top ? m0 - 1 : m0 + r; hn = top ? n0 + r : n0 - 1;
-                rm = top ? m0 : hm;         rn = top ? hn : n0;
+                hm = top ? m0 - 1 : m0 + hr; hn = top ? n0 + hr : n0 - 1;
+                rm = top ? m0 : hm;          rn = top ? hn : n0;
             }
             const bool r_inner = rm < M && rn < N && interior(rm, rn);
             const bool need = own_edge ? (inner || (valid && r_inner)) : (hm >= 0 && hn >= 0 && r_inner);
@@ -237,8 +278,11 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
                 const R o1 = own_edge ? (uv ? own[3] : own[2]) : src[h + MNL * (2 + uv)];
                 const R p = own_edge ? (e == 0 ? own[5] : e == 1 ? own[6] : e == 2 ? own[7] : own[8])
                                      : src[h + MNL * (5 + dir + 2 * uv)];
-                g = edge_grad<R>(tab, P.K2, P.epsn, P.lams, P.guard != 0, T, a, u1,
-                                 src[r + MNL * uv], o1, src[r + MNL * (2 + uv)], p);
+                const R o2 = src[r + MNL * (2 + uv)];
+                const EdgeCoef<R> c = edge_coef(u1, src[r + MNL * uv], o1, o2, p);
+                Sums<R> S = edge_sums(tab, kj, K2, Q, P.epsn, c);
+                if (Q > 1) S = lane_combine<Q>(S);
+                g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p);
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
@@ -248,22 +292,21 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
                 eE = eE + g.E;
                 eda = eda + g.da;
                 // neighbour share: (m+1,n) reads in_up, (m,n+1) reads in_left
-                if (dir == 0 && lm + 1 < TILE) { in_up[uv][0][tid + 1] = g.du2; in_up[uv][1][tid + 1] = g.do2; }
-                if (dir == 1 && ln + 1 < TILE) { in_left[uv][0][tid + TILE] = g.du2; in_left[uv][1][tid + TILE] = g.do2; }
-            } else {
-                const int r = tid & 15;
-                if (dir == 0) { in_up[uv][0][r * TILE] = g.du2; in_up[uv][1][r * TILE] = g.do2; }
-                else          { in_left[uv][0][r] = g.du2; in_left[uv][1][r] = g.do2; }
+                if (lead && dir == 0 && lm + 1 < TM) { in_up[uv][0][pix + 1] = g.du2; in_up[uv][1][pix + 1] = g.do2; }
+                if (lead && dir == 1 && ln + 1 < TM) { in_left[uv][0][pix + TM] = g.du2; in_left[uv][1][pix + TM] = g.do2; }
+            } else if (tid % Q == 0) {
+                if (dir == 0) { in_up[uv][0][hr * TM] = g.du2; in_up[uv][1][hr * TM] = g.do2; }
+                else          { in_left[uv][0][hr] = g.du2; in_left[uv][1][hr] = g.do2; }
             }
         }
         __syncthreads();
         fix128 fda = 0;
-        if (inner) {
+        if (inner && lead) {
             // dmuu = dmuu + sum(dmu1(:,:,:,:,1),4) + circshift(dmu2(..1,1),1) + circshift(dmu2(..2,1),1,2)
-            const R gmu_u = ((nd.du1 + sum_mu0) + in_up[0][0][tid]) + in_left[0][0][tid];
-            const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][tid]) + in_left[1][0][tid];
-            const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][tid]) + in_left[0][1][tid];
-            const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][tid]) + in_left[1][1][tid];
+            const R gmu_u = ((nd.du1 + sum_mu0) + in_up[0][0][pix]) + in_left[0][0][pix];
+            const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][pix]) + in_left[1][0][pix];
+            const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][pix]) + in_left[0][1][pix];
+            const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
             dst[i + MNL * 0] = cl(own[0] + gmu_u * step, P.minu, P.maxu);
             dst[i + MNL * 1] = cl(own[1] + gmu_v * step, P.minv, P.maxv);
@@ -496,16 +539,30 @@ struct gqmap_ctx {
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
+    int split = 1;      // lanes per node (Q): 1, 4 or 16
     hipGraphExec_t graph = nullptr;
     double tab_host[NTAB * TS];
 };
 
 namespace {
 
+// Lanes per node: enough lanes for >= 2^17 (8 waves per SIMD... at least
+// 2 per SIMD) on a 256-CU part; the full-resolution 584x388 grid needs none.
+int choose_split(int M, int N, int forced)
+{
+    if (forced == 1 || forced == 4 || forced == 16) return forced;
+    const int64_t nodes = (int64_t)M * N;
+    if (nodes >= (1 << 17)) return 1;
+    if (nodes * 4 >= (1 << 17)) return 4;
+    return 16;
+}
+
 gqmap_status alloc_grid(gqmap_ctx *c)
 {
-    c->tiles_m = (c->M + TILE - 1) / TILE;
-    c->tiles_n = (c->N + TILE - 1) / TILE;
+    c->split = choose_split(c->M, c->N, c->opt.split);
+    const int tile = c->split == 1 ? 16 : c->split == 4 ? 8 : 4;
+    c->tiles_m = (c->M + tile - 1) / tile;
+    c->tiles_n = (c->N + tile - 1) / tile;
     c->nblocks = c->tiles_m * c->tiles_n;
     const size_t bytes = (size_t)c->MNL * NPLANES * c->rsz;
     for (int b = 0; b < 2; ++b) {
@@ -562,7 +619,12 @@ FinParams fin_params(const gqmap_ctx *c)
 template <typename R, typename VT, bool SUPER>
 void launch_iter_t(gqmap_ctx *c)
 {
-    k_iter<R, VT, SUPER><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+    if (c->split == 16)
+        k_iter<R, VT, SUPER, 16><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+    else if (c->split == 4)
+        k_iter<R, VT, SUPER, 4><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+    else
+        k_iter<R, VT, SUPER, 1><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
 }
 
 void launch_iter(gqmap_ctx *c)
@@ -1001,7 +1063,7 @@ gqmap_status gqmap_get_info(gqmap_ctx *c, gqmap_info *info)
     DeviceGuard dg(c->device);
     std::memset(info, 0, sizeof(*info));
     info->Mo = c->Mo; info->No = c->No; info->M = c->M; info->N = c->N;
-    info->L = c->L; info->K = c->K; info->device = c->device;
+    info->L = c->L; info->K = c->K; info->device = c->device; info->split = c->split;
     if (c->have_state) {
         Ctl h;
         gqmap_status s = read_ctl(c, &h);

@@ -337,43 +337,100 @@ GQ_HD Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s, R t, 
     return g;
 }
 
+// Sums over a split quadrature: lane j of Q accumulates k = j, j+Q, ... in
+// increasing k; the Q partial sums are combined by an xor butterfly
+// (offsets Q/2, ..., 1): total = ((p0+p_{Q/2}) + ...) -- butterfly() below is
+// the reference evaluation of that order, the kernel does it with shuffles.
+template <typename R>
+GQ_HD Sums<R> sums_plus(const Sums<R> &a, const Sums<R> &b)
+{
+    Sums<R> r;
+    r.s0 = a.s0 + b.s0; r.sxi = a.sxi + b.sxi; r.sxj = a.sxj + b.sxj;
+    r.sa = a.sa + b.sa; r.sm = a.sm + b.sm; r.sx = a.sx + b.sx;
+    return r;
+}
+template <typename R>
+GQ_HD Sums<R> butterfly(const Sums<R> *parts, int Q)
+{
+    Sums<R> v[16];
+    for (int j = 0; j < Q; ++j) v[j] = parts[j];
+    for (int o = Q / 2; o > 0; o >>= 1) {
+        Sums<R> w[16];
+        for (int j = 0; j < Q; ++j) w[j] = sums_plus(v[j], v[j ^ o]);
+        for (int j = 0; j < Q; ++j) v[j] = w[j];
+    }
+    return v[0];
+}
+
 // edge_grad_spectral (gqmap_gpu_mixture.m:118-146) with edge_pot (:180-182):
 // x1 - x2 = sqrt2*o1*(s XI + t XJ) + u1 - sqrt2*o2*(t XI + s XJ) - u2
+template <typename R>
+struct EdgeCoef {
+    R s, t, A, B, C;
+};
+template <typename R>
+GQ_HD EdgeCoef<R> edge_coef(R u1, R u2, R o1, R o2, R p)
+{
+    EdgeCoef<R> c;
+    spectral_st(p, c.s, c.t);
+    const R sq2 = R(GQ_M_SQRT2);
+    c.A = sq2 * (o1 * c.s - o2 * c.t);
+    c.B = sq2 * (o1 * c.t - o2 * c.s);
+    c.C = u1 - u2;
+    return c;
+}
+template <typename R, typename TP>
+GQ_HD Sums<R> edge_sums(TP tab, int k0, int K2, int dk, R eps, const EdgeCoef<R> &c)
+{
+    Sums<R> S;
+    GQ_UNROLL2
+    for (int k = k0; k < K2; k += dk) {
+        const R d = fma(c.A, tab[k], fma(c.B, tab[TAB_STRIDE + k], c.C));
+        S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+    }
+    return S;
+}
+template <typename R>
+GQ_HD Grad<R> edge_epi(const Sums<R> &S, const EdgeCoef<R> &c, R lams, bool guard, R T, R a, R o1,
+                       R o2, R p)
+{
+    return epilogue(S, -lams, a, o1, o2, p, c.s, c.t, T, !guard || a != R(0));
+}
 template <typename R, typename TP>
 GQ_HD Grad<R> edge_grad(TP tab, int K2, R eps, R lams, bool guard, R T, R a, R u1, R u2, R o1,
                         R o2, R p)
 {
-    R s, t;
-    spectral_st(p, s, t);
-    const R sq2 = R(GQ_M_SQRT2);
-    const R A = sq2 * (o1 * s - o2 * t), B = sq2 * (o1 * t - o2 * s), C = u1 - u2;
-    Sums<R> S;
-    GQ_UNROLL2
-    for (int k = 0; k < K2; ++k) {
-        const R d = fma(A, tab[k], fma(B, tab[TAB_STRIDE + k], C));
-        S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
-    }
-    return epilogue(S, -lams, a, o1, o2, p, s, t, T, !guard || a != R(0));
+    const EdgeCoef<R> c = edge_coef(u1, u2, o1, o2, p);
+    return edge_epi(edge_sums(tab, 0, K2, 1, eps, c), c, lams, guard, T, a, o1, o2, p);
 }
 
 // node_grad_spectral (gqmap_gpu_mixture.m:87-116; super: gqmap_gpuSuper_mix_entropy.m:87-122).
 // (m, n) 0-based node; single-scale reads pixel (m, n), super the 4x4 block.
-template <bool SUPER, typename R, typename TP, typename VP, typename IP>
-GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R eps, R lamd,
-                        bool guard, R T, R a, R u1, R u2, R o1, R o2, R p, int m, int n)
+template <typename R>
+struct NodeCoef {
+    R s, t, ax, bx, ay, by;  // x1 = ax XI + bx XJ + u1, x2 = ay XI + by XJ + u2
+};
+template <typename R>
+GQ_HD NodeCoef<R> node_coef(R o1, R o2, R p)
 {
-    R s, t;
-    spectral_st(p, s, t);
+    NodeCoef<R> c;
+    spectral_st(p, c.s, c.t);
     const R sq2 = R(GQ_M_SQRT2);
-    const R ax = sq2 * o1 * s, bx = sq2 * o1 * t;  // x1 = ax XI + bx XJ + u1
-    const R ay = sq2 * o2 * t, by = sq2 * o2 * s;  // x2 = ay XI + by XJ + u2
+    c.ax = sq2 * o1 * c.s; c.bx = sq2 * o1 * c.t;
+    c.ay = sq2 * o2 * c.t; c.by = sq2 * o2 * c.s;
+    return c;
+}
+template <bool SUPER, typename R, typename TP, typename VP, typename IP>
+GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, int Mo, int No,
+                        R eps, const NodeCoef<R> &c, R u1, R u2, int m, int n)
+{
     Sums<R> S;
     if (!SUPER) {
         const R I = I1[m + (int64_t)Mo * n];
         GQ_NODE_UNROLL
-        for (int k = 0; k < K2; ++k) {
-            const R x1 = fma(ax, tab[k], fma(bx, tab[TAB_STRIDE + k], u1));
-            const R x2 = fma(ay, tab[k], fma(by, tab[TAB_STRIDE + k], u2));
+        for (int k = k0; k < K2; k += dk) {
+            const R x1 = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], u1));
+            const R x2 = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], u2));
             const R d = I - sample(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
             S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
         }
@@ -382,13 +439,27 @@ GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R 
         R I[16];
         const int i0 = 4 * m, j0 = 4 * n;  // 0-based top-left pixel of the block
         for (int q = 0; q < 16; ++q) I[q] = I1[(i0 + (q >> 2)) + (int64_t)Mo * (j0 + (q & 3))];
-        for (int k = 0; k < K2; ++k) {
-            const R x1 = fma(ax, tab[k], fma(bx, tab[TAB_STRIDE + k], u1));
-            const R x2 = fma(ay, tab[k], fma(by, tab[TAB_STRIDE + k], u2));
+        for (int k = k0; k < K2; k += dk) {
+            const R x1 = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], u1));
+            const R x2 = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], u2));
             S.add(tab, k, super_block_sum<R>(VV, M2, Mo, No, i0, j0, x1, x2, eps, I));
         }
     }
-    return epilogue(S, -lamd, a, o1, o2, p, s, t, R(-3) * T, !guard || a != R(0));
+    return S;
+}
+template <typename R>
+GQ_HD Grad<R> node_epi(const Sums<R> &S, const NodeCoef<R> &c, R lamd, bool guard, R T, R a, R o1,
+                       R o2, R p)
+{
+    return epilogue(S, -lamd, a, o1, o2, p, c.s, c.t, R(-3) * T, !guard || a != R(0));
+}
+template <bool SUPER, typename R, typename TP, typename VP, typename IP>
+GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R eps, R lamd,
+                        bool guard, R T, R a, R u1, R u2, R o1, R o2, R p, int m, int n)
+{
+    const NodeCoef<R> c = node_coef(o1, o2, p);
+    return node_epi(node_sums<SUPER>(tab, 0, K2, 1, VV, I1, M2, Mo, No, eps, c, u1, u2, m, n), c,
+                    lamd, guard, T, a, o1, o2, p);
 }
 
 }  // namespace gq

@@ -27,7 +27,7 @@ from .ops import flow_to_color
 ENGINES = {"mixture": _lib.ENGINE_MIXTURE, "super": _lib.ENGINE_SUPER}
 PRECISIONS = {"fp64": _lib.FP64, "fp32": _lib.FP32}
 KNOBS = ("alpha_mode", "alpha_start", "alpha_lr", "guard_a", "t_decay_every", "t_min", "step0",
-         "step_decay", "sig_lo", "sig_hi", "corr_tor", "tor")
+         "step_decay", "sig_lo", "sig_hi", "corr_tor", "tor", "split")
 
 
 def make_options(options: dict, engine: str = "mixture", precision: str = "fp64") -> _lib.GqmapOptions:

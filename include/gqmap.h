@@ -79,6 +79,8 @@ typedef struct gqmap_options {
     double sig_lo, sig_hi;  /* 0.01 / 23 mixture (:43-44), 0.01 / 25 super       */
     double corr_tor;     /* 1-1e-5 (:7)                                          */
     double tor;          /* 1e-4 stop threshold on ptdmu (:25,75)                */
+    int split;           /* lanes per node Q (1/4/16), 0 = auto from the grid size;
+                            part of the arithmetic (partial quadrature sums)    */
 } gqmap_options;
 
 /* Engine state, MATLAB layout (M x N x L [x 2 x 2]).  M,N = node grid
@@ -101,6 +103,7 @@ typedef struct gqmap_info {
     int stopped;         /* ptdmu < tor reached */
     double T;
     int device;
+    int split;           /* lanes per node Q in use                             */
 } gqmap_info;
 
 typedef struct gqmap_ctx gqmap_ctx;

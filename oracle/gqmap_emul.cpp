@@ -56,9 +56,20 @@ struct Work {
 inline bool interior(int m, int n, int M, int N) { return m >= 1 && m <= M - 2 && n >= 1 && n <= N - 2; }
 inline bool finite_d(double x) { return std::isfinite(x); }
 
+// one term's quadrature sum split over Q lanes (k = j, j+Q, ...) + butterfly
+template <typename F>
+auto split_sums(int Q, F part) -> decltype(part(0, 1))
+{
+    if (Q == 1) return part(0, 1);
+    decltype(part(0, 1)) parts[16];
+    for (int j = 0; j < Q; ++j) parts[j] = part(j, Q);
+    return butterfly(parts, Q);
+}
+
 template <typename R, bool SUPER>
 int run_t(const orc_params *P, const double *X, const double *W, const double *I1,
-          const double *VV, orc_state *S, double *T_io, int it_first, int n_iter, double *trace)
+          const double *VV, orc_state *S, double *T_io, int it_first, int n_iter, double *trace,
+          int Q)
 {
     Work<R> w;
     w.P = P;
@@ -117,11 +128,15 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                 for (int m = 0; m < M; ++m) {
                     const int64_t i = m + (int64_t)M * n + MN * l;
                     const bool inner = interior(m, n, M, N);
-                    if (inner)
-                        w.node[i] = node_grad<SUPER, R>(tab, w.K2, VVp, I1p, w.M2, w.Mo, w.No, eps,
-                                                        lamd, guard, Tr, a, st[i], st[i + MNL],
-                                                        st[i + 2 * MNL], st[i + 3 * MNL],
-                                                        st[i + 4 * MNL], m, n);
+                    if (inner) {
+                        const NodeCoef<R> c = node_coef(st[i + 2 * MNL], st[i + 3 * MNL], st[i + 4 * MNL]);
+                        const Sums<R> Sn = split_sums(Q, [&](int k0, int dk) {
+                            return node_sums<SUPER>(tab, k0, w.K2, dk, VVp, I1p, w.M2, w.Mo, w.No, eps,
+                                                    c, st[i], st[i + MNL], m, n);
+                        });
+                        w.node[i] = node_epi(Sn, c, lamd, guard, Tr, a, st[i + 2 * MNL],
+                                             st[i + 3 * MNL], st[i + 4 * MNL]);
+                    }
                     for (int e = 0; e < 4; ++e) {
                         const int dir = e & 1, uv = e >> 1;
                         const int rm = dir == 0 ? m + 1 : m, rn = dir == 1 ? n + 1 : n;
@@ -129,9 +144,13 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                         Grad<R> g{};
                         if (inner || r_inner) {
                             const int64_t r = rm + (int64_t)M * rn + MN * l;
-                            g = edge_grad<R>(tab, w.K2, eps, lams, guard, Tr, a, st[i + MNL * uv],
-                                             st[r + MNL * uv], st[i + MNL * (2 + uv)],
-                                             st[r + MNL * (2 + uv)], st[i + MNL * (5 + e)]);
+                            const R o1 = st[i + MNL * (2 + uv)], o2 = st[r + MNL * (2 + uv)];
+                            const R p = st[i + MNL * (5 + e)];
+                            const EdgeCoef<R> c = edge_coef(st[i + MNL * uv], st[r + MNL * uv], o1, o2, p);
+                            const Sums<R> Se = split_sums(Q, [&](int k0, int dk) {
+                                return edge_sums(tab, k0, w.K2, dk, eps, c);
+                            });
+                            g = edge_epi(Se, c, lams, guard, Tr, a, o1, o2, p);
                         }
                         w.edge[i * 4 + e] = g;
                     }
@@ -250,16 +269,18 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
 
 extern "C" int emu_run(const orc_params *P, const double *X, const double *W, const double *I1,
                        const double *VV, orc_state *S, double *T_io, int it_first, int n_iter,
-                       double *trace, int nthreads, int fp32)
+                       double *trace, int nthreads, int fp32, int split)
 {
+    const int Q = split;
+    if (Q != 1 && Q != 4 && Q != 16) return -2;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
     if (P->super_)
-        return fp32 ? run_t<float, true>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace)
-                    : run_t<double, true>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace);
-    return fp32 ? run_t<float, false>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace)
-                : run_t<double, false>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace);
+        return fp32 ? run_t<float, true>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
+                    : run_t<double, true>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
+    return fp32 ? run_t<float, false>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
+                : run_t<double, false>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
 }
 
 extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)

@@ -206,8 +206,14 @@ def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0) -> np.ndarray:
     return out
 
 
+def split_for(M: int, N: int) -> int:
+    """The library's default lanes-per-node policy (gqmap_engine.hip choose_split)."""
+    nodes = M * N
+    return 1 if nodes >= (1 << 17) else 4 if nodes * 4 >= (1 << 17) else 16
+
+
 def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
-            T: float | None = None, nthreads: int = 0, fp32: bool = False):
+            T: float | None = None, nthreads: int = 0, fp32: bool = False, split: int | None = None):
     """CPU model of the HIP kernel (oracle/gqmap_emul.cpp): bit-identical to
     libgqmap.so for the same quadrature nodes X, W (pass the product's
     gauss_hermite(K)).  Returns (done, trace[done,3], T)."""
@@ -221,8 +227,9 @@ def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
     cs = state.cstruct()
     f = lib().emu_run
     f.restype = C.c_int
+    Q = int(opts.get("split", 0)) or (split_for(p.M, p.N) if split is None else split)
     done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
-             _p(trace), nthreads, int(fp32))
+             _p(trace), nthreads, int(fp32), Q)
     if done < 0:
         raise RuntimeError("emu_run failed")
     return done, trace[:done].copy(), Tbox[0]

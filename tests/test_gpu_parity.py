@@ -156,12 +156,13 @@ def _gh(K):
     return gauss_hermite(K)
 
 
-def _emulate(o, I1, I2, st, its, precision):
+def _emulate(o, I1, I2, st, its, precision, split):
     from oracle import oracle
     ost = _oracle_state(st)
     X, W = _gh(o["K"])
     done, tr, T = oracle.emu_run(o, I1, I2, ost, st.it, its, X, W, T=st.T,
-                                 nthreads=min(16, os.cpu_count() or 1), fp32=precision == "fp32")
+                                 nthreads=min(16, os.cpu_count() or 1), fp32=precision == "fp32",
+                                 split=split)
     return done, tr, T, ost
 
 
@@ -179,28 +180,36 @@ def test_bit_exact_vs_emulator_golden_init(name, precision):
     d = G.load(name)
     o = d["opts"]
     st = State(**G.state(d), it=1, T=o["temperature"])
-    e_done, e_tr, e_T, ost = _emulate(o, d["I1"], d["I2"], st, 25, precision)
     with _engine(d, precision) as eng:
         eng.set_state(State(**G.state(d), it=1, T=o["temperature"]))
         done, tr = eng.run(25)
         g = eng.get_state()
+        split = eng.info().split
+    e_done, e_tr, e_T, ost = _emulate(o, d["I1"], d["I2"], st, 25, precision, split)
     _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
     assert g.T == e_T
 
 
 @pytest.mark.parametrize("precision", ["fp64", "fp32"])
-@pytest.mark.parametrize("engine,L,K,M,N", [("mixture", 1, 9, 96, 128), ("mixture", 3, 9, 70, 90),
-                                            ("super", 3, 11, 96, 128)])
-def test_bit_exact_vs_emulator_reference_init(engine, L, K, M, N, precision):
+@pytest.mark.parametrize("engine,L,K,M,N,split", [("mixture", 1, 9, 96, 128, 1),
+                                                  ("mixture", 1, 9, 96, 128, 4),
+                                                  ("mixture", 3, 9, 70, 90, 16),
+                                                  ("mixture", 3, 9, 70, 90, 1),
+                                                  ("super", 3, 11, 96, 128, 16),
+                                                  ("super", 3, 11, 96, 128, 4),
+                                                  ("super", 1, 11, 100, 132, 1)])
+def test_bit_exact_vs_emulator_reference_init(engine, L, K, M, N, split, precision):
     # reference-style init (pn = rou = 0), many tiles (halo edges across tiles),
-    # ragged last tiles, alpha update from iteration 10
+    # ragged last tiles, alpha update from iteration 10, every lanes-per-node Q
     from gqmap_opticalflow_amd import Engine
     I1, I2, _, _, o, st = _reference_init_case("rubberwhale", M, N, 150, 200, L=L, K=K,
-                                               engine=engine, alpha_start=10, t_decay_every=20)
-    e_done, e_tr, e_T, ost = _emulate(o, I1, I2, st, 60, precision)
+                                               engine=engine, alpha_start=10, t_decay_every=20,
+                                               split=split)
+    e_done, e_tr, e_T, ost = _emulate(o, I1, I2, st, 40, precision, split)
     with Engine(o, I1, I2, engine, precision) as eng:
+        assert eng.info().split == split
         eng.set_state(st)
-        done, tr = eng.run(60)
+        done, tr = eng.run(40)
         g = eng.get_state()
     _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
 
@@ -213,8 +222,9 @@ def test_full_rubberwhale_500_iterations_bit_exact():
     from gqmap_opticalflow_amd import Engine, aepe
     I1, I2, flo, unk, o, st = _reference_init_case("rubberwhale", 388, 584)
     its = 500
-    e_done, e_tr, _, ost = _emulate(o, I1, I2, st, its, "fp64")
+    e_done, e_tr, _, ost = _emulate(o, I1, I2, st, its, "fp64", 1)
     with Engine(o, I1, I2) as eng:
+        assert eng.info().split == 1
         eng.set_state(st)
         done, tr = eng.run(its)
         g = eng.get_state()
