@@ -15,7 +15,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GQMAP_LIB", os.path.join(PKG_DIR, "libgqmap.so"))
 
 GQMAP_OK = 0
-ENGINE_MIXTURE, ENGINE_SUPER = 0, 1
+ENGINE_MIXTURE, ENGINE_SUPER, ENGINE_CTF = 0, 1, 2
 FP64, FP32 = 0, 1
 ALPHA_SOFTMAX, ALPHA_PROJSPLX = 0, 1
 LMAX, KMAX = 8, 16
@@ -41,7 +41,7 @@ class GqmapOptions(C.Structure):
         ("guard_a", C.c_int), ("t_decay_every", C.c_int), ("t_min", C.c_double),
         ("step0", C.c_double), ("step_decay", C.c_double),
         ("sig_lo", C.c_double), ("sig_hi", C.c_double), ("corr_tor", C.c_double),
-        ("tor", C.c_double), ("split", C.c_int),
+        ("tor", C.c_double), ("split", C.c_int), ("sig_step", C.c_double), ("sig_init", C.c_double),
     ]
 
 

@@ -107,7 +107,7 @@ struct IterParams {
     int M, N, Mo, No, M2, L, K2;
     int tiles_m, tiles_n;
     R epsn, lamd, lams;
-    R minu, maxu, minv, maxv, sig_lo, sig_hi, corr;
+    R minu, maxu, minv, maxv, sig_lo, sig_hi, corr, sig_step;
     double step0, step_decay;
     int guard;
     int64_t MNL;
@@ -169,7 +169,7 @@ __device__ __forceinline__ Sums<R> lane_combine(Sums<R> S)
 // Lane j of a node sums the quadrature points k = j, j+Q, ... and the lanes
 // combine with an xor butterfly (the spec's butterfly()).
 // ---------------------------------------------------------------------------
-template <typename R, typename VT, bool SUPER, int Q>
+template <typename R, typename VT, int ENG, int Q>
 __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> P)
 {
     constexpr int TPIX = BLOCK / Q;                   // nodes per tile
@@ -234,10 +234,10 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
         if (inner && own[0] == R(12345.678)) {  // timing ablation only
 #endif
             const NodeCoef<R> c = node_coef(own[2], own[3], own[4]);
-            Sums<R> S = node_sums<SUPER>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
-                                         own[0], own[1], m, n);
+            Sums<R> S = node_sums<ENG>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
+                                       own[0], own[1], m, n);
             if (Q > 1) S = lane_combine<Q>(S);
-            nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, own[2], own[3], own[4]);
+            nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, own[2], own[3], own[4], ENG == 2);
         }
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
         // edges, then job 4 on the halo lanes: the edges entering the tile from
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
                 const EdgeCoef<R> c = edge_coef(u1, src[r + MNL * uv], o1, o2, p);
                 Sums<R> S = edge_sums(tab, kj, K2, Q, P.epsn, c);
                 if (Q > 1) S = lane_combine<Q>(S);
-                g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p);
+                g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p, ENG == 2);
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
@@ -310,8 +310,11 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
             dst[i + MNL * 0] = cl(own[0] + gmu_u * step, P.minu, P.maxu);
             dst[i + MNL * 1] = cl(own[1] + gmu_v * step, P.minv, P.maxv);
-            dst[i + MNL * 2] = cl(own[2] + gsg_u * step, P.sig_lo, P.sig_hi);
-            dst[i + MNL * 3] = cl(own[3] + gsg_v * step, P.sig_lo, P.sig_hi);
+            // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
+            const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
+            const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
+            dst[i + MNL * 2] = cl(own[2] + su, P.sig_lo, P.sig_hi);
+            dst[i + MNL * 3] = cl(own[3] + sv, P.sig_lo, P.sig_hi);
             dst[i + MNL * 4] = cl(own[4] + nd.dp * step, -P.corr, P.corr);
             dst[i + MNL * 5] = cl(own[5] + drou0 * step, -P.corr, P.corr);
             dst[i + MNL * 6] = cl(own[6] + drou1 * step, -P.corr, P.corr);
@@ -440,13 +443,16 @@ __global__ __launch_bounds__(256) void k_finalize(FinParams F)
 
 template <typename R>
 __global__ void k_init_state(R *st0, R *st1, int64_t MNL, uint64_t b1, uint64_t b2, uint64_t b3,
-                             uint64_t b4, double minu, double maxu, double minv, double maxv)
+                             uint64_t b4, double minu, double maxu, double minv, double maxv,
+                             double sig_init)
 {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= MNL) return;
-    // gqmap_gpu_mixture.m:19-24 (no contraction: same bits as the host formula)
+    // gqmap_gpu_mixture.m:19-24 (gqmap_ctf.m:14-17: sigma = rand + 3); no
+    // contraction: same bits as the host formula
+    const double su = sig_init < 0 ? maxu - minu : sig_init, sv = sig_init < 0 ? maxv - minv : sig_init;
     const R v[NPLANES] = {R(minu + u01(b1, i) * (maxu - minu)), R(minv + u01(b2, i) * (maxv - minv)),
-                          R(u01(b3, i) + (maxu - minu)),        R(u01(b4, i) + (maxv - minv)),
+                          R(u01(b3, i) + su),                   R(u01(b4, i) + sv),
                           R(0), R(0), R(0), R(0), R(0)};
 #pragma unroll
     for (int q = 0; q < NPLANES; ++q) {
@@ -594,6 +600,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.epsn = R(o.epsn); P.lamd = R(o.lambdad); P.lams = R(o.lambdas);
     P.minu = R(o.minu); P.maxu = R(o.maxu); P.minv = R(o.minv); P.maxv = R(o.maxv);
     P.sig_lo = R(o.sig_lo); P.sig_hi = R(o.sig_hi); P.corr = R(o.corr_tor);
+    P.sig_step = R(o.sig_step);
     P.step0 = o.step0; P.step_decay = o.step_decay;
     P.guard = o.guard_a;
     P.MNL = c->MNL;
@@ -616,29 +623,32 @@ FinParams fin_params(const gqmap_ctx *c)
     return F;
 }
 
-template <typename R, typename VT, bool SUPER>
-void launch_iter_t(gqmap_ctx *c)
+template <typename R, typename VT, int ENG>
+void launch_iter_q(gqmap_ctx *c)
 {
     if (c->split == 16)
-        k_iter<R, VT, SUPER, 16><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+        k_iter<R, VT, ENG, 16><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
     else if (c->split == 4)
-        k_iter<R, VT, SUPER, 4><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+        k_iter<R, VT, ENG, 4><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
     else
-        k_iter<R, VT, SUPER, 1><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+        k_iter<R, VT, ENG, 1><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+}
+
+template <typename R, typename VT>
+void launch_iter_t(gqmap_ctx *c)
+{
+    switch (c->opt.engine) {
+    case GQMAP_ENGINE_SUPER: launch_iter_q<R, VT, 1>(c); break;
+    case GQMAP_ENGINE_CTF: launch_iter_q<R, VT, 2>(c); break;
+    default: launch_iter_q<R, VT, 0>(c); break;
+    }
 }
 
 void launch_iter(gqmap_ctx *c)
 {
-    if (c->fp32) {
-        if (c->super_) launch_iter_t<float, float, true>(c);
-        else launch_iter_t<float, float, false>(c);
-    } else if (c->vv32) {
-        if (c->super_) launch_iter_t<double, float, true>(c);
-        else launch_iter_t<double, float, false>(c);
-    } else {
-        if (c->super_) launch_iter_t<double, double, true>(c);
-        else launch_iter_t<double, double, false>(c);
-    }
+    if (c->fp32) launch_iter_t<float, float>(c);
+    else if (c->vv32) launch_iter_t<double, float>(c);
+    else launch_iter_t<double, double>(c);
 }
 
 void launch_finalize(gqmap_ctx *c) { k_finalize<<<1, 256, 0, c->stream>>>(fin_params(c)); }
@@ -733,6 +743,24 @@ void gqmap_options_default(gqmap_options *o, int engine)
 {
     std::memset(o, 0, sizeof(*o));
     const bool sup = engine == GQMAP_ENGINE_SUPER;
+    if (engine == GQMAP_ENGINE_CTF) {
+        // legacy/optical_flow_ctf.m:13-17 + legacy/gqmap_ctf.m constants
+        o->its = 3000; o->K = 11; o->L = 1;
+        o->temperature = 0.0; o->drate = 0.5;
+        o->epsn = 1e-6; o->lambdad = 1.0; o->lambdas = 5.0;
+        o->minu = -1; o->maxu = 1; o->minv = -1; o->maxv = 1;
+        o->engine = engine; o->precision = GQMAP_FP64;
+        o->alpha_mode = GQMAP_ALPHA_SOFTMAX; o->alpha_start = 1 << 30; o->alpha_lr = 0;
+        o->guard_a = 0; o->t_decay_every = 0; o->t_min = 0.0;
+        o->step0 = 0.07;         /* constant step (:27) */
+        o->step_decay = 1e300;   /* step0/(1+it/1e300) == step0 exactly */
+        o->sig_lo = 0.01; o->sig_hi = 25.0;   /* :34-35 */
+        o->corr_tor = 0.999;     /* :5 */
+        o->tor = 1e-4;
+        o->sig_step = 0.3;       /* sigma step x0.3 (:34-35) */
+        o->sig_init = 3.0;       /* sigma = rand + 3 (:16-17) */
+        return;
+    }
     // driver values: optical_flow.m:16-23 / optical_flowSuper.m:19-26
     o->its = 30000;
     o->K = sup ? 11 : 9;
@@ -757,6 +785,8 @@ void gqmap_options_default(gqmap_options *o, int engine)
     o->sig_hi = sup ? 25.0 : 23.0;
     o->corr_tor = 1 - 1e-5;
     o->tor = 1e-4;
+    o->sig_step = 1.0;
+    o->sig_init = -1.0;  /* sigma = rand + (max-min) (gqmap_gpu_mixture.m:21-22) */
 }
 
 gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
@@ -768,8 +798,11 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
              opt->L, GQMAP_LMAX);
     GQ_CHECK(opt->K >= 2 && opt->K <= GQMAP_KMAX, GQMAP_ERR_INVALID_ARG, "K=%d outside [2,%d]",
              opt->K, GQMAP_KMAX);
-    GQ_CHECK(opt->engine == GQMAP_ENGINE_MIXTURE || opt->engine == GQMAP_ENGINE_SUPER,
+    GQ_CHECK(opt->engine == GQMAP_ENGINE_MIXTURE || opt->engine == GQMAP_ENGINE_SUPER ||
+                 opt->engine == GQMAP_ENGINE_CTF,
              GQMAP_ERR_INVALID_ARG, "unknown engine %d", opt->engine);
+    GQ_CHECK(opt->engine != GQMAP_ENGINE_CTF || opt->L == 1, GQMAP_ERR_INVALID_ARG,
+             "the coarse-to-fine engine is single-Gaussian (L=1)");
     GQ_CHECK(opt->precision == GQMAP_FP64 || opt->precision == GQMAP_FP32, GQMAP_ERR_INVALID_ARG,
              "unknown precision %d", opt->precision);
     GQ_CHECK(opt->minu <= opt->maxu && opt->minv <= opt->maxv, GQMAP_ERR_INVALID_ARG,
@@ -895,10 +928,10 @@ gqmap_status gqmap_init_state(gqmap_ctx *c, uint64_t seed)
     const uint64_t b3 = stream_base(seed, 3), b4 = stream_base(seed, 4);
     if (c->fp32)
         k_init_state<float><<<blocks, threads, 0, c->stream>>>(
-            (float *)c->d_st[0], (float *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv);
+            (float *)c->d_st[0], (float *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv, o.sig_init);
     else
         k_init_state<double><<<blocks, threads, 0, c->stream>>>(
-            (double *)c->d_st[0], (double *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv);
+            (double *)c->d_st[0], (double *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv, o.sig_init);
     GQ_HIP(hipGetLastError());
     double w[GQMAP_LMAX], alpha[GQMAP_LMAX], se = 0;
     gqmap_rand_uniform(seed, 0, 0, (size_t)c->L, w);  // w = rand(1,1,L)

@@ -20,7 +20,8 @@
 //
 // Reference lines this arithmetic restates: node_pot / edge_pot
 // (gqmap_gpu_mixture.m:156-182), node/edge_grad_spectral (:87-146), super
-// node sum (gqmap_gpuSuper_mix_entropy.m:94-105).
+// node sum (gqmap_gpuSuper_mix_entropy.m:94-105), coarse-to-fine level
+// (legacy/gqmap_ctf.m:79-150).
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -209,6 +210,25 @@ GQ_HD float sample(VP VV, int M2, int Mo, int No, int ii, int jj, float x1, floa
     return bicubic_cell<float>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, so, to);
 }
 
+// Coarse-to-fine level data term (legacy/gqmap_ctf.m:10, 96):
+//   I2_cont(clamp(round((m+x2-1)*64+1),1,MM), clamp(round((n+x1-1)*64+1),1,NN))
+// with I2_cont = interp2(I2,6,'cubic') the 64x-refined cubic table.  A table
+// entry (r, c) is the same Keys interpolation at (1+(c-1)/64, 1+(r-1)/64), so
+// the lookup is sample() at the position rounded to the 1/64 grid -- the
+// 64x table (10 GB at 480x640) is never built.
+template <typename VP, typename R>
+GQ_HD R sample_ctf(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+{
+    const R MM = R(64 * (Mo - 1) + 1), NN = R(64 * (No - 1) + 1);
+    const R ry = fmin(fmax(round((((R)ii + x2) - R(1)) * R(64) + R(1)), R(1)), MM);
+    const R rx = fmin(fmax(round((((R)jj + x1) - R(1)) * R(64) + R(1)), R(1)), NN);
+    const R Yq = (ry - R(1)) * R(0.015625) + R(1), Xq = (rx - R(1)) * R(0.015625) + R(1);
+    int ix = (int)Xq, iy = (int)Yq;  // Xq in [1, No]: truncation == floor
+    ix = ix > No - 1 ? No - 1 : ix;
+    iy = iy > Mo - 1 ? Mo - 1 : iy;
+    return bicubic_cell<R>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, Xq - (R)ix, Yq - (R)iy);
+}
+
 // ---------------------------------------------------------------------------
 // 4x4 super-pixel data term (gqmap_gpuSuper_mix_entropy.m:94-105):
 //   sum_{i=top..bottom} sum_{j=left..right} sqrt(eps + (I1(i,j) - interp(j+x1, i+x2))^2)
@@ -308,7 +328,7 @@ GQ_HD void spectral_st(R p, R &s, R &t)
 // (gqmap_gpu_mixture.m:107-115 and :137-145).  lam = -lambda scales the sums.
 template <typename R>
 GQ_HD Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s, R t, R tau,
-                       bool live)
+                       bool live, bool raw_energy = false)
 {
     const R pi = R(GQ_M_PI);
     const R c1 = R(2.8378770664093454835606594728112);  // 1 + log(2*pi)
@@ -333,7 +353,8 @@ GQ_HD Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s, R t, 
     g.do1 = a * (do1 / pi + tau) / o1;
     g.do2 = a * (do2 / pi + tau) / o2;
     g.dp = a * (dp / pi - tau * p) / pr;
-    g.E = a * g.da;
+    // gqmap_ctf.m's nener/eener = -lambda*sum(fval): no 1/pi, no alpha
+    g.E = raw_energy ? S0 : a * g.da;
     return g;
 }
 
@@ -392,9 +413,9 @@ GQ_HD Sums<R> edge_sums(TP tab, int k0, int K2, int dk, R eps, const EdgeCoef<R>
 }
 template <typename R>
 GQ_HD Grad<R> edge_epi(const Sums<R> &S, const EdgeCoef<R> &c, R lams, bool guard, R T, R a, R o1,
-                       R o2, R p)
+                       R o2, R p, bool raw_energy = false)
 {
-    return epilogue(S, -lams, a, o1, o2, p, c.s, c.t, T, !guard || a != R(0));
+    return epilogue(S, -lams, a, o1, o2, p, c.s, c.t, T, !guard || a != R(0), raw_energy);
 }
 template <typename R, typename TP>
 GQ_HD Grad<R> edge_grad(TP tab, int K2, R eps, R lams, bool guard, R T, R a, R u1, R u2, R o1,
@@ -420,18 +441,21 @@ GQ_HD NodeCoef<R> node_coef(R o1, R o2, R p)
     c.ay = sq2 * o2 * c.t; c.by = sq2 * o2 * c.s;
     return c;
 }
-template <bool SUPER, typename R, typename TP, typename VP, typename IP>
+// ENG: 0 single-scale mixture, 1 super (4x4 blocks), 2 coarse-to-fine level
+template <int ENG, typename R, typename TP, typename VP, typename IP>
 GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, int Mo, int No,
                         R eps, const NodeCoef<R> &c, R u1, R u2, int m, int n)
 {
     Sums<R> S;
-    if (!SUPER) {
+    if (ENG != 1) {
         const R I = I1[m + (int64_t)Mo * n];
         GQ_NODE_UNROLL
         for (int k = k0; k < K2; k += dk) {
             const R x1 = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], u1));
             const R x2 = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], u2));
-            const R d = I - sample(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
+            const R v = ENG == 2 ? sample_ctf(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
+                                 : sample(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
+            const R d = I - v;
             S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
         }
     } else {
@@ -449,17 +473,17 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
 }
 template <typename R>
 GQ_HD Grad<R> node_epi(const Sums<R> &S, const NodeCoef<R> &c, R lamd, bool guard, R T, R a, R o1,
-                       R o2, R p)
+                       R o2, R p, bool raw_energy = false)
 {
-    return epilogue(S, -lamd, a, o1, o2, p, c.s, c.t, R(-3) * T, !guard || a != R(0));
+    return epilogue(S, -lamd, a, o1, o2, p, c.s, c.t, R(-3) * T, !guard || a != R(0), raw_energy);
 }
-template <bool SUPER, typename R, typename TP, typename VP, typename IP>
+template <int ENG, typename R, typename TP, typename VP, typename IP>
 GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R eps, R lamd,
                         bool guard, R T, R a, R u1, R u2, R o1, R o2, R p, int m, int n)
 {
     const NodeCoef<R> c = node_coef(o1, o2, p);
-    return node_epi(node_sums<SUPER>(tab, 0, K2, 1, VV, I1, M2, Mo, No, eps, c, u1, u2, m, n), c,
-                    lamd, guard, T, a, o1, o2, p);
+    return node_epi(node_sums<ENG>(tab, 0, K2, 1, VV, I1, M2, Mo, No, eps, c, u1, u2, m, n), c,
+                    lamd, guard, T, a, o1, o2, p, ENG == 2);
 }
 
 }  // namespace gq

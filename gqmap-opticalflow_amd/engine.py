@@ -24,10 +24,10 @@ from . import _lib
 from ._lib import check, dptr, f64
 from .ops import flow_to_color
 
-ENGINES = {"mixture": _lib.ENGINE_MIXTURE, "super": _lib.ENGINE_SUPER}
+ENGINES = {"mixture": _lib.ENGINE_MIXTURE, "super": _lib.ENGINE_SUPER, "ctf": _lib.ENGINE_CTF}
 PRECISIONS = {"fp64": _lib.FP64, "fp32": _lib.FP32}
 KNOBS = ("alpha_mode", "alpha_start", "alpha_lr", "guard_a", "t_decay_every", "t_min", "step0",
-         "step_decay", "sig_lo", "sig_hi", "corr_tor", "tor", "split")
+         "step_decay", "sig_lo", "sig_hi", "corr_tor", "tor", "split", "sig_step", "sig_init")
 
 
 def make_options(options: dict, engine: str = "mixture", precision: str = "fp64") -> _lib.GqmapOptions:
@@ -89,7 +89,8 @@ def rand_uniform(seed: int, stream: int, n: int, first: int = 0) -> np.ndarray:
     return out
 
 
-def initial_state(options: dict, M: int, N: int, seed: int = 0, T: float | None = None) -> State:
+def initial_state(options: dict, M: int, N: int, seed: int = 0, T: float | None = None,
+                  engine: str = "mixture") -> State:
     """Host copy of gqmap_init_state: gqmap_gpu_mixture.m:18-24 with the
     library RNG (what the device generates for the same seed)."""
     L = int(options["L"])
@@ -97,11 +98,14 @@ def initial_state(options: dict, M: int, N: int, seed: int = 0, T: float | None 
     sh = lambda a: a.reshape((M, N, L), order="F")
     w = rand_uniform(seed, 0, L)
     du, dv = options["maxu"] - options["minu"], options["maxv"] - options["minv"]
+    # sigma offset: (max-min) for the mixture engines, 3 for ctf (gqmap_ctf.m:16-17)
+    sig_init = float(options.get("sig_init", 3.0 if engine == "ctf" else -1.0))
+    su, sv = (du, dv) if sig_init < 0 else (sig_init, sig_init)
     st = State(
         muu=sh(options["minu"] + rand_uniform(seed, 1, MNL) * du),
         muv=sh(options["minv"] + rand_uniform(seed, 2, MNL) * dv),
-        sigu=sh(rand_uniform(seed, 3, MNL) + du),
-        sigv=sh(rand_uniform(seed, 4, MNL) + dv),
+        sigu=sh(rand_uniform(seed, 3, MNL) + su),
+        sigv=sh(rand_uniform(seed, 4, MNL) + sv),
         pn=np.zeros((M, N, L), order="F"), rou=np.zeros((M, N, L, 2, 2), order="F"),
         w=w, alpha=np.exp(w) / np.exp(w).sum(), it=1,
         T=float(options.get("temperature", 0.0) if T is None else T))

@@ -48,7 +48,8 @@ typedef enum gqmap_status {
 
 typedef enum gqmap_engine_kind {
     GQMAP_ENGINE_MIXTURE = 0,  /* gqmap_gpu_mixture.m: one node per pixel          */
-    GQMAP_ENGINE_SUPER = 1     /* gqmap_gpuSuper_mix_entropy.m: one node per 4x4   */
+    GQMAP_ENGINE_SUPER = 1,    /* gqmap_gpuSuper_mix_entropy.m: one node per 4x4   */
+    GQMAP_ENGINE_CTF = 2       /* legacy/gqmap_ctf.m: one pyramid level, L=1       */
 } gqmap_engine_kind;
 
 typedef enum gqmap_precision { GQMAP_FP64 = 0, GQMAP_FP32 = 1 } gqmap_precision;
@@ -81,6 +82,8 @@ typedef struct gqmap_options {
     double tor;          /* 1e-4 stop threshold on ptdmu (:25,75)                */
     int split;           /* lanes per node Q (1/4/16), 0 = auto from the grid size;
                             part of the arithmetic (partial quadrature sums)    */
+    double sig_step;     /* sigma step scale: 1, ctf 0.3 (gqmap_ctf.m:34-35)     */
+    double sig_init;     /* init sigma = U + sig_init; < 0: U + (max - min)      */
 } gqmap_options;
 
 /* Engine state, MATLAB layout (M x N x L [x 2 x 2]).  M,N = node grid

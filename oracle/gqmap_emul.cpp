@@ -66,7 +66,7 @@ auto split_sums(int Q, F part) -> decltype(part(0, 1))
     return butterfly(parts, Q);
 }
 
-template <typename R, bool SUPER>
+template <typename R, int ENG>
 int run_t(const orc_params *P, const double *X, const double *W, const double *I1,
           const double *VV, orc_state *S, double *T_io, int it_first, int n_iter, double *trace,
           int Q)
@@ -110,6 +110,7 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
     const R eps = R(P->epsn), lamd = R(P->lambdad), lams = R(P->lambdas);
     const R minu = R(P->minu), maxu = R(P->maxu), minv = R(P->minv), maxv = R(P->maxv);
     const R sig_lo = R(P->sig_lo), sig_hi = R(P->sig_hi), corr = R(P->corr_tor);
+    const R sig_step = R(P->sig_step);
     const bool guard = P->guard_a != 0;
     const R *tab = w.tab.data();
     const R *VVp = w.VV.data();
@@ -131,11 +132,11 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                     if (inner) {
                         const NodeCoef<R> c = node_coef(st[i + 2 * MNL], st[i + 3 * MNL], st[i + 4 * MNL]);
                         const Sums<R> Sn = split_sums(Q, [&](int k0, int dk) {
-                            return node_sums<SUPER>(tab, k0, w.K2, dk, VVp, I1p, w.M2, w.Mo, w.No, eps,
-                                                    c, st[i], st[i + MNL], m, n);
+                            return node_sums<ENG>(tab, k0, w.K2, dk, VVp, I1p, w.M2, w.Mo, w.No, eps,
+                                                  c, st[i], st[i + MNL], m, n);
                         });
                         w.node[i] = node_epi(Sn, c, lamd, guard, Tr, a, st[i + 2 * MNL],
-                                             st[i + 3 * MNL], st[i + 4 * MNL]);
+                                             st[i + 3 * MNL], st[i + 4 * MNL], ENG == 2);
                     }
                     for (int e = 0; e < 4; ++e) {
                         const int dir = e & 1, uv = e >> 1;
@@ -150,7 +151,7 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                             const Sums<R> Se = split_sums(Q, [&](int k0, int dk) {
                                 return edge_sums(tab, k0, w.K2, dk, eps, c);
                             });
-                            g = edge_epi(Se, c, lams, guard, Tr, a, o1, o2, p);
+                            g = edge_epi(Se, c, lams, guard, Tr, a, o1, o2, p, ENG == 2);
                         }
                         w.edge[i * 4 + e] = g;
                     }
@@ -186,8 +187,10 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                         R *ns = w.nst.data();
                         ns[i + MNL * 0] = cl(st[i] + gmu_u * step, minu, maxu);
                         ns[i + MNL * 1] = cl(st[i + MNL] + gmu_v * step, minv, maxv);
-                        ns[i + MNL * 2] = cl(st[i + 2 * MNL] + gsg_u * step, sig_lo, sig_hi);
-                        ns[i + MNL * 3] = cl(st[i + 3 * MNL] + gsg_v * step, sig_lo, sig_hi);
+                        const R su = ENG == 2 ? (gsg_u * step) * sig_step : gsg_u * step;
+                        const R sv = ENG == 2 ? (gsg_v * step) * sig_step : gsg_v * step;
+                        ns[i + MNL * 2] = cl(st[i + 2 * MNL] + su, sig_lo, sig_hi);
+                        ns[i + MNL * 3] = cl(st[i + 3 * MNL] + sv, sig_lo, sig_hi);
                         ns[i + MNL * 4] = cl(st[i + 4 * MNL] + nd.dp * step, -corr, corr);
                         for (int e = 0; e < 4; ++e)
                             ns[i + MNL * (5 + e)] = cl(st[i + MNL * (5 + e)] + ed[e].dp * step, -corr, corr);
@@ -276,11 +279,14 @@ extern "C" int emu_run(const orc_params *P, const double *X, const double *W, co
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
+    if (P->ctf)
+        return fp32 ? run_t<float, 2>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
+                    : run_t<double, 2>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
     if (P->super_)
-        return fp32 ? run_t<float, true>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
-                    : run_t<double, true>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
-    return fp32 ? run_t<float, false>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
-                : run_t<double, false>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
+        return fp32 ? run_t<float, 1>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
+                    : run_t<double, 1>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
+    return fp32 ? run_t<float, 0>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
+                : run_t<double, 0>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
 }
 
 extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)

@@ -74,8 +74,19 @@ def interp_cubic(VV, M, N, Xq, Yq):
     return Vq / 4
 
 
+def matlab_round(v):
+    """MATLAB round: half away from zero (exact: v - trunc(v) is exact)."""
+    r = np.trunc(v)
+    return r + np.where(np.abs(v - r) >= 0.5, np.sign(v), 0.0)
+
+
 class Engine:
     def __init__(self, opts: dict, I1: np.ndarray, I2: np.ndarray):
+        self.ctf = opts.get("engine", "mixture") == "ctf"
+        if self.ctf:  # legacy/gqmap_ctf.m constants
+            opts = dict(dict(step0=0.07, step_decay=1e300, sig_hi=25.0, corr_tor=0.999,
+                             guard_a=0, alpha_start=1 << 30, t_decay_every=0, t_min=0.0, temperature=0.0,
+                             sig_step=0.3), **opts)
         self.o = opts
         self.sup = opts.get("engine", "mixture") == "super"
         self.I1 = np.asarray(I1, dtype=np.float64)
@@ -97,6 +108,14 @@ class Engine:
     # --- potentials -------------------------------------------------
     def node_pot(self, x1, x2, ms, ns):
         o = self.o
+        if self.ctf:
+            # gqmap_ctf.m:96 lookup into I2_cont = interp2(I2,6,'cubic'), returned
+            # WITHOUT -lambda (the ctf gradients apply -lambda at the end)
+            MM, NN = 64 * (self.Mo - 1) + 1, 64 * (self.No - 1) + 1
+            r = np.clip(matlab_round((ms + x2 - 1) * 64 + 1), 1, MM)
+            c = np.clip(matlab_round((ns + x1 - 1) * 64 + 1), 1, NN)
+            Vq = interp_cubic(self.VV, self.Mo, self.No, (c - 1) / 64 + 1, (r - 1) / 64 + 1)
+            return np.sqrt(o["epsn"] + (self.I1[ms - 1, ns - 1] - Vq) ** 2)
         if not self.sup:
             Vq = interp_cubic(self.VV, self.Mo, self.No, ns + x1, ms + x2)
             I = self.I1[ms - 1, ns - 1]
@@ -111,7 +130,15 @@ class Engine:
         return tot
 
     def edge_pot(self, x1, x2):
+        if self.ctf:
+            return np.sqrt(self.o["epsn"] + (x1 - x2) ** 2)
         return -self.o["lambdas"] * np.sqrt(self.o["epsn"] + (x1 - x2) ** 2)
+
+    def _ctf_epi(self, acc, pr, lam, o1, o2):
+        # legacy/gqmap_ctf.m:104-109 and :144-149
+        return (np.zeros_like(o1), -lam * acc["du1"] * (SQRT2 / (o1 * pr)) / np.pi,
+                -lam * acc["du2"] * (SQRT2 / (o2 * pr)) / np.pi, -lam * acc["do1"] / np.pi / o1,
+                -lam * acc["do2"] / np.pi / o2, -lam * acc["dp"] / np.pi / pr, -lam * acc["Ei"])
 
     def _spectral(self, pot_fn, a, u1, u2, o1, o2, p):
         q = self.q
@@ -140,6 +167,8 @@ class Engine:
         const1 = 1 + np.log(2 * np.pi)
         acc, pr, sqrtpr = self._spectral(lambda x1, x2: self.node_pot(x1, x2, ms, ns),
                                          a, u1, u2, o1, o2, p)
+        if self.ctf:
+            return self._ctf_epi(acc, pr, self.o["lambdad"], o1, o2)
         du1 = a * acc["du1"] * (SQRT2 / (o1 * pr)) / np.pi
         du2 = a * acc["du2"] * (SQRT2 / (o2 * pr)) / np.pi
         da = acc["Ei"] / np.pi - 3 * T * (const1 + np.log(sqrtpr * o1 * o2))
@@ -151,6 +180,8 @@ class Engine:
     def edge_grad(self, T, a, u1, u2, o1, o2, p):
         const1 = 1 + np.log(2 * np.pi)
         acc, pr, sqrtpr = self._spectral(self.edge_pot, a, u1, u2, o1, o2, p)
+        if self.ctf:
+            return self._ctf_epi(acc, pr, self.o["lambdas"], o1, o2)
         du1 = a * acc["du1"] * (SQRT2 / (o1 * pr)) / np.pi
         du2 = a * acc["du2"] * (SQRT2 / (o2 * pr)) / np.pi
         da = acc["Ei"] / np.pi + T * (const1 + np.log(sqrtpr * o1 * o2))
@@ -197,8 +228,13 @@ class Engine:
         cl = lambda x, lo, hi: np.minimum(np.maximum(x, lo), hi)
         st["muu"][I, J] = cl(st["muu"][I, J] + dmuu[I, J] * step, o["minu"], o["maxu"])
         st["muv"][I, J] = cl(st["muv"][I, J] + dmuv[I, J] * step, o["minv"], o["maxv"])
-        st["sigu"][I, J] = cl(st["sigu"][I, J] + dsigu[I, J] * step, self.sig_lo, self.sig_hi)
-        st["sigv"][I, J] = cl(st["sigv"][I, J] + dsigv[I, J] * step, self.sig_lo, self.sig_hi)
+        if self.ctf:  # gqmap_ctf.m:34-35: dsigmau*step*0.3
+            f = float(o.get("sig_step", 0.3))
+            st["sigu"][I, J] = cl(st["sigu"][I, J] + dsigu[I, J] * step * f, self.sig_lo, self.sig_hi)
+            st["sigv"][I, J] = cl(st["sigv"][I, J] + dsigv[I, J] * step * f, self.sig_lo, self.sig_hi)
+        else:
+            st["sigu"][I, J] = cl(st["sigu"][I, J] + dsigu[I, J] * step, self.sig_lo, self.sig_hi)
+            st["sigv"][I, J] = cl(st["sigv"][I, J] + dsigv[I, J] * step, self.sig_lo, self.sig_hi)
         st["rou"][I, J] = cl(st["rou"][I, J] + drou[I, J] * step, -self.corr, self.corr)
         st["pn"][I, J] = cl(st["pn"][I, J] + dpn[I, J] * step, -self.corr, self.corr)
         energy = nE[I, J].sum() + eE[I, J].sum()

@@ -172,6 +172,82 @@ static inline double node_pot(const orc_ctx *c, double x1, double x2, int i, int
     return -c->p->lambdad * sqrt(c->p->epsn + d * d);
 }
 
+/* legacy/gqmap_ctf.m:96: I2_cont(clamp(round((m+x2-1)*rfc2+1),1,MM), clamp(round((n+x1-1)*rfc2+1),1,NN))
+ * with I2_cont = interp2(I2,6,'cubic'); entry (r,c) of the 64x-refined table is
+ * the cubic interpolation at (1+(c-1)/64, 1+(r-1)/64), evaluated here directly. */
+static inline double ctf_lookup(const orc_ctx *c, double x1, double x2, int m, int n)
+{
+    const int Mo = c->p->Mo, No = c->p->No;
+    const double rfc2 = 64.0, MM = 64.0 * (Mo - 1) + 1, NN = 64.0 * (No - 1) + 1;
+    const double r = fmin(fmax(round((m + x2 - 1) * rfc2 + 1), 1.0), MM);
+    const double cc = fmin(fmax(round((n + x1 - 1) * rfc2 + 1), 1.0), NN);
+    return orc_interp_cubic(c->VV, Mo, No, (cc - 1) / rfc2 + 1, (r - 1) / rfc2 + 1);
+}
+
+/* node_grad_spectral of legacy/gqmap_ctf.m:79-110 (no mixture weight, no entropy) */
+static void ctf_node_grad(const orc_ctx *c, double u1, double u2, double o1, double o2, double p,
+                          int m, int n, double *out)
+{
+    const orc_params *P = c->p;
+    double du1 = 0, du2 = 0, do1 = 0, do2 = 0, dp = 0, nener = 0;
+    const double s = (sqrt(1 + p) + sqrt(1 - p)) / 2;
+    const double t = (sqrt(1 + p) - sqrt(1 - p)) / 2;
+    const double pr = 1 - p * p, sqrtpr = sqrt(pr);
+    const double o1pr = SQRT2 / (o1 * pr), o2pr = SQRT2 / (o2 * pr);
+    const double I = c->I1[(m - 1) + (size_t)P->Mo * (n - 1)];
+    for (int k = 0; k < c->K2; ++k) {
+        const double zi = s * c->XI[k] + t * c->XJ[k], zj = t * c->XI[k] + s * c->XJ[k];
+        const double x1 = SQRT2 * o1 * zi + u1, x2 = SQRT2 * o2 * zj + u2;
+        const double d = I - ctf_lookup(c, x1, x2, m, n);
+        const double fval = c->WIWJ[k] * sqrt(P->epsn + d * d);
+        dp = dp + fval * (p - p * c->XI2aXJ2[k] + 2 * c->XIXJ[k]);
+        du1 = du1 + fval * (zi - p * zj);
+        du2 = du2 + fval * (zj - p * zi);
+        do1 = do1 + fval * (c->XI2aXJ2[k] - 1 + c->XI2mXJ2[k] / sqrtpr);
+        do2 = do2 + fval * (c->XI2aXJ2[k] - 1 - c->XI2mXJ2[k] / sqrtpr);
+        nener = nener + fval;
+    }
+    const double lam = P->lambdad;
+    out[0] = 0;
+    out[1] = -lam * du1 * o1pr / M_PI;
+    out[2] = -lam * du2 * o2pr / M_PI;
+    out[3] = -lam * do1 / M_PI / o1;
+    out[4] = -lam * do2 / M_PI / o2;
+    out[5] = -lam * dp / M_PI / pr;
+    out[6] = -lam * nener;
+}
+
+/* edge_grad_spectral of legacy/gqmap_ctf.m:128-150 */
+static void ctf_edge_grad(const orc_ctx *c, double u1, double u2, double o1, double o2, double p,
+                          double *out)
+{
+    const orc_params *P = c->p;
+    double du1 = 0, du2 = 0, do1 = 0, do2 = 0, dp = 0, eener = 0;
+    const double s = (sqrt(1 + p) + sqrt(1 - p)) / 2;
+    const double t = (sqrt(1 + p) - sqrt(1 - p)) / 2;
+    const double pr = 1 - p * p, sqrtpr = sqrt(pr);
+    const double o1pr = SQRT2 / (o1 * pr), o2pr = SQRT2 / (o2 * pr);
+    for (int k = 0; k < c->K2; ++k) {
+        const double zi = s * c->XI[k] + t * c->XJ[k], zj = t * c->XI[k] + s * c->XJ[k];
+        const double d = SQRT2 * o1 * zi + u1 - SQRT2 * o2 * zj - u2;
+        const double fval = c->WIWJ[k] * sqrt(P->epsn + d * d);
+        dp = dp + fval * (p - p * c->XI2aXJ2[k] + 2 * c->XIXJ[k]);
+        du1 = du1 + fval * (zi - p * zj);
+        du2 = du2 + fval * (zj - p * zi);
+        do1 = do1 + fval * (c->XI2aXJ2[k] - 1 + c->XI2mXJ2[k] / sqrtpr);
+        do2 = do2 + fval * (c->XI2aXJ2[k] - 1 - c->XI2mXJ2[k] / sqrtpr);
+        eener = eener + fval;
+    }
+    const double lam = P->lambdas;
+    out[0] = 0;
+    out[1] = -lam * du1 * o1pr / M_PI;
+    out[2] = -lam * du2 * o2pr / M_PI;
+    out[3] = -lam * do1 / M_PI / o1;
+    out[4] = -lam * do2 / M_PI / o2;
+    out[5] = -lam * dp / M_PI / pr;
+    out[6] = -lam * eener;
+}
+
 /* edge_pot, gqmap_gpu_mixture.m:180-182 */
 static inline double edge_pot(const orc_ctx *c, double x1, double x2)
 {
@@ -272,8 +348,12 @@ static void eval_grads(const orc_ctx *c, const orc_state *st, double T, double *
         for (int l = 0; l < L; ++l)
             for (int m = 0; m < M; ++m) {
                 const size_t i = m + (size_t)M * n + MN * l;
-                node_grad(c, T, st->alpha[l], st->muu[i], st->muv[i], st->sigu[i], st->sigv[i],
-                          st->pn[i], m + 1, n + 1, o);
+                if (P->ctf)
+                    ctf_node_grad(c, st->muu[i], st->muv[i], st->sigu[i], st->sigv[i], st->pn[i],
+                                  m + 1, n + 1, o);
+                else
+                    node_grad(c, T, st->alpha[l], st->muu[i], st->muv[i], st->sigu[i], st->sigv[i],
+                              st->pn[i], m + 1, n + 1, o);
                 for (int q = 0; q < 7; ++q) node[q * MNL + i] = o[q];
                 for (int dir = 0; dir < 2; ++dir) {
                     /* circshift(X,-1): row m+1 (wrap); circshift(X,-1,2): col n+1 (wrap) */
@@ -284,7 +364,8 @@ static void eval_grads(const orc_ctx *c, const orc_state *st, double T, double *
                         const double *mu = uv == 0 ? st->muu : st->muv;
                         const double *sg = uv == 0 ? st->sigu : st->sigv;
                         const size_t e = i + MNL * (dir + 2 * uv);
-                        edge_grad(c, T, st->alpha[l], mu[i], mu[j], sg[i], sg[j], st->rou[e], o);
+                        if (P->ctf) ctf_edge_grad(c, mu[i], mu[j], sg[i], sg[j], st->rou[e], o);
+                        else edge_grad(c, T, st->alpha[l], mu[i], mu[j], sg[i], sg[j], st->rou[e], o);
                         for (int q = 0; q < 7; ++q) edge[q * MNL * 4 + e] = o[q];
                     }
                 }
@@ -376,8 +457,13 @@ int orc_run(const orc_params *P, const double *I1, const double *VV, orc_state *
                     const size_t i = m + (size_t)M * n + MN * l;
                     st->muu[i] = clampd(st->muu[i] + g[0][i] * step, P->minu, P->maxu);
                     st->muv[i] = clampd(st->muv[i] + g[1][i] * step, P->minv, P->maxv);
-                    st->sigu[i] = clampd(st->sigu[i] + g[2][i] * step, P->sig_lo, P->sig_hi);
-                    st->sigv[i] = clampd(st->sigv[i] + g[3][i] * step, P->sig_lo, P->sig_hi);
+                    if (P->ctf) { /* gqmap_ctf.m:34-35: dsigmau*step*0.3 */
+                        st->sigu[i] = clampd(st->sigu[i] + g[2][i] * step * P->sig_step, P->sig_lo, P->sig_hi);
+                        st->sigv[i] = clampd(st->sigv[i] + g[3][i] * step * P->sig_step, P->sig_lo, P->sig_hi);
+                    } else {
+                        st->sigu[i] = clampd(st->sigu[i] + g[2][i] * step, P->sig_lo, P->sig_hi);
+                        st->sigv[i] = clampd(st->sigv[i] + g[3][i] * step, P->sig_lo, P->sig_hi);
+                    }
                     for (int e = 0; e < 4; ++e)
                         st->rou[i + MNL * e] = clampd(st->rou[i + MNL * e] + drou[i + MNL * e] * step,
                                                       -P->corr_tor, P->corr_tor);

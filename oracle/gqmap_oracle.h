@@ -37,6 +37,8 @@ typedef struct {
     int alpha_start;     /* alpha update when it > alpha_start (:50)           */
     double alpha_lr;     /* 1e-7                                               */
     double tor;          /* stop when ptdmu < tor (:75)                        */
+    int ctf;             /* 1: legacy/gqmap_ctf.m level solver (rounded I2_cont lookup) */
+    double sig_step;     /* sigma step scale (ctf: 0.3, gqmap_ctf.m:34-35)     */
 } orc_params;
 
 typedef struct {

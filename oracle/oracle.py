@@ -29,7 +29,7 @@ class OrcParams(C.Structure):
         ("step0", C.c_double), ("step_decay", C.c_double),
         ("sig_lo", C.c_double), ("sig_hi", C.c_double), ("corr_tor", C.c_double),
         ("alpha_mode", C.c_int), ("alpha_start", C.c_int), ("alpha_lr", C.c_double),
-        ("tor", C.c_double),
+        ("tor", C.c_double), ("ctf", C.c_int), ("sig_step", C.c_double),
     ]
 
 
@@ -91,7 +91,13 @@ def interp_cubic(VV: np.ndarray, M: int, N: int, Xq: float, Yq: float) -> float:
 def make_params(opts: dict, Mo: int, No: int) -> OrcParams:
     """opts uses the reference option names plus the engine knobs of
     gqmap_opticalflow_amd.options (engine, step0, ...)."""
-    sup = opts.get("engine", "mixture") == "super"
+    eng = opts.get("engine", "mixture")
+    sup = eng == "super"
+    if eng == "ctf":
+        # legacy/gqmap_ctf.m constants (see gqmap_options_default)
+        opts = dict(dict(step0=0.07, step_decay=1e300, sig_hi=25.0, corr_tor=0.999, guard_a=0,
+                         alpha_start=1 << 30, t_decay_every=0, t_min=0.0, temperature=0.0, L=1,
+                         sig_step=0.3), **opts)
     p = OrcParams()
     p.Mo, p.No = Mo, No
     p.M, p.N = (Mo // 4, No // 4) if sup else (Mo, No)
@@ -114,6 +120,8 @@ def make_params(opts: dict, Mo: int, No: int) -> OrcParams:
     p.alpha_start = int(opts.get("alpha_start", 500))
     p.alpha_lr = float(opts.get("alpha_lr", 1e-7))
     p.tor = float(opts.get("tor", 1e-4))
+    p.ctf = int(eng == "ctf")
+    p.sig_step = float(opts.get("sig_step", 1.0))
     return p
 
 

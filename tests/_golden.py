@@ -5,7 +5,7 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ("mixture_L1", "mixture_L3_T", "mixture_L3_proj", "super_L3")
+CASES = ("mixture_L1", "mixture_L3_T", "mixture_L3_proj", "super_L3", "ctf_L1")
 STATE_KEYS = ("muu", "muv", "sigu", "sigv", "pn", "rou", "w", "alpha")
 
 

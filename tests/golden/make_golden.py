@@ -25,8 +25,8 @@ from oracle import gqmap_np  # noqa: E402
 from gqmap_opticalflow_amd.flowio import load_pair  # noqa: E402
 
 
-def crop_pair(r0, c0, M, N):
-    I1, I2, gt = load_pair("rubberwhale")
+def crop_pair(r0, c0, M, N, name="rubberwhale"):
+    I1, I2, gt = load_pair(name)
     return (np.asfortranarray(I1[r0:r0 + M, c0:c0 + N]), np.asfortranarray(I2[r0:r0 + M, c0:c0 + N]),
             np.asfortranarray(gt[r0:r0 + M, c0:c0 + N]))
 
@@ -57,12 +57,15 @@ CASES = {
     "super_L3": dict(engine="super", crop=(100, 240, 32, 40), K=11, L=3, temperature=0.2,
                      drate=0.75, lambdas=16.0, lambdad=1.0, its=3, seed=4, alpha_start=1,
                      alpha_lr=1e-4, t_decay_every=2),
+    # coarse-to-fine level solver (legacy/gqmap_ctf.m), K=11 as optical_flow_ctf.m:13
+    "ctf_L1": dict(engine="ctf", crop=(200, 300, 22, 30), K=11, L=1, temperature=0.0,
+                   lambdas=5.0, lambdad=1.0, its=3, seed=5, pair="Grove3"),
 }
 
 
 def make_case(name, c):
     r0, c0, M, N = c["crop"]
-    I1, I2, gt = crop_pair(r0, c0, M, N)
+    I1, I2, gt = crop_pair(r0, c0, M, N, c.get("pair", "rubberwhale"))
     # minu..maxv come from flowToColor of the GT (unknown pixels zeroed), optical_flow.m:12-13
     _, _, (minu, maxu, minv, maxv), _ = gqmap_np.flow_to_color(gt)
     opts = dict(engine=c["engine"], K=c["K"], L=c["L"], temperature=c["temperature"],

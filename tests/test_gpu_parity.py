@@ -98,14 +98,16 @@ def test_chunked_runs_and_graph_replay_are_bit_identical():
             np.testing.assert_array_equal(getattr(sa, k), getattr(sb, k))
 
 
-def test_device_init_equals_host_init():
+@pytest.mark.parametrize("name", ["mixture_L3_T", "ctf_L1"])
+def test_device_init_equals_host_init(name):
     from gqmap_opticalflow_amd import Engine, initial_state
-    d = G.load("mixture_L3_T")
+    d = G.load(name)
     o = d["opts"]
-    with Engine(o, d["I1"], d["I2"]) as eng:
+    eng_name = o.get("engine", "mixture")
+    with Engine(o, d["I1"], d["I2"], eng_name) as eng:
         eng.init_state(seed=11)
         st = eng.get_state()
-    ref = initial_state(o, d["I1"].shape[0], d["I1"].shape[1], seed=11)
+    ref = initial_state(o, d["I1"].shape[0], d["I1"].shape[1], seed=11, engine=eng_name)
     for k in G.STATE_KEYS:
         np.testing.assert_array_equal(getattr(st, k), getattr(ref, k))
     assert st.it == 1 and st.T == o["temperature"]
@@ -136,11 +138,14 @@ def _reference_init_case(name, M, N, r0=0, c0=0, L=1, K=9, engine="mixture", **e
     gt = gt[r0:r0 + M, c0:c0 + N]
     _, flo, (minu, maxu, minv, maxv), unk = gqmap_np.flow_to_color(gt)
     sup = engine == "super"
+    if engine == "ctf":
+        # pyramid levels see resampled (non-integer) frames: exercises the fp64 VV store
+        I1 = np.asfortranarray(I1 * 0.7); I2 = np.asfortranarray(I2 * 0.7 + 0.1)
     o = dict(engine=engine, K=K, L=L, temperature=0.2 if sup else 0.0, drate=0.75 if sup else 0.5,
              epsn=1e-6, lambdad=1.0, lambdas=16.0 if sup else 5.0,
              minu=minu, maxu=maxu, minv=minv, maxv=maxv, **extra)
     Mn, Nn = (M // 4, N // 4) if sup else (M, N)
-    st = initial_state(o, Mn, Nn, seed=0)
+    st = initial_state(o, Mn, Nn, seed=0, engine=engine)
     return I1, I2, flo, unk, o, st
 
 
@@ -197,7 +202,10 @@ def test_bit_exact_vs_emulator_golden_init(name, precision):
                                                   ("mixture", 3, 9, 70, 90, 1),
                                                   ("super", 3, 11, 96, 128, 16),
                                                   ("super", 3, 11, 96, 128, 4),
-                                                  ("super", 1, 11, 100, 132, 1)])
+                                                  ("super", 1, 11, 100, 132, 1),
+                                                  ("ctf", 1, 11, 96, 128, 1),
+                                                  ("ctf", 1, 11, 60, 70, 4),
+                                                  ("ctf", 1, 11, 30, 44, 16)])
 def test_bit_exact_vs_emulator_reference_init(engine, L, K, M, N, split, precision):
     # reference-style init (pn = rou = 0), many tiles (halo edges across tiles),
     # ragged last tiles, alpha update from iteration 10, every lanes-per-node Q
