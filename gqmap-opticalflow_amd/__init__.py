@@ -5,9 +5,11 @@ interface and driver scripts."""
 from .engine import (Engine, State, aepe, gqmap_gpu_mixture, gqmap_gpuSuper_mix_entropy,
                      initial_state, make_options, rand_uniform)
 from .flowio import load_pair, read_flow_file, rgb2gray, write_flow_file
-from .ops import flow_to_color, gauss_hermite, mixture_map, projsplx
+from .ops import flow_to_color, gauss_hermite, imresize, mixture_map, projsplx, resize_len, warp_image
+from .pyramid import C3_SCALES, REFERENCE_SCALES, Pyramid, ctf_options, gqmap_ctf, optical_flow_ctf
 
 __all__ = ["Engine", "State", "aepe", "gqmap_gpu_mixture", "gqmap_gpuSuper_mix_entropy",
            "initial_state", "make_options", "rand_uniform", "load_pair", "read_flow_file",
            "rgb2gray", "write_flow_file", "flow_to_color", "gauss_hermite", "mixture_map",
-           "projsplx"]
+           "projsplx", "imresize", "resize_len", "warp_image", "Pyramid", "gqmap_ctf",
+           "optical_flow_ctf", "ctf_options", "C3_SCALES", "REFERENCE_SCALES"]

@@ -26,8 +26,11 @@ EXPORTS = (
     "gqmap_set_state", "gqmap_get_state", "gqmap_run", "gqmap_run_timed", "gqmap_get_info",
     "gqmap_get_map", "gqmap_log_p", "gqmap_synchronize", "gqmap_destroy", "gqmap_projsplx",
     "gqmap_mixture_map", "gqmap_flow_to_color", "gqmap_gauss_hermite", "gqmap_rand_uniform",
-    "gqmap_last_error", "gqmap_abi_version", "gqmap_device_count",
+    "gqmap_last_error", "gqmap_abi_version", "gqmap_device_count", "gqmap_imresize",
+    "gqmap_warp_image", "gqmap_ctf_create", "gqmap_ctf_set_images", "gqmap_ctf_run",
+    "gqmap_ctf_get_level", "gqmap_ctf_destroy", "gqmap_resize_len",
 )
+CTF_MAX_LEVELS = 8
 
 
 class GqmapOptions(C.Structure):
@@ -100,6 +103,14 @@ def load():
         "gqmap_last_error": (C.c_char_p, []),
         "gqmap_abi_version": (C.c_int, []),
         "gqmap_device_count": (C.c_int, []),
+        "gqmap_imresize": (C.c_int, [_D, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int, _D, C.c_int]),
+        "gqmap_warp_image": (C.c_int, [_D, C.c_int, C.c_int, _D, C.c_int, _D, C.c_int]),
+        "gqmap_ctf_create": (C.c_int, [P(vp), P(GqmapOptions), _D, C.c_int, C.c_int]),
+        "gqmap_ctf_set_images": (C.c_int, [vp, _D, _D, C.c_int, C.c_int]),
+        "gqmap_ctf_run": (C.c_int, [vp, C.c_uint64, _D, P(C.c_int), _D]),
+        "gqmap_ctf_get_level": (C.c_int, [vp, C.c_int, P(C.c_int), P(C.c_int), _D, _D, _D, _D]),
+        "gqmap_ctf_destroy": (None, [vp]),
+        "gqmap_resize_len": (C.c_int, [C.c_int, C.c_double]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -547,6 +547,7 @@ struct gqmap_ctx {
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
     int split = 1;      // lanes per node (Q): 1, 4 or 16
     hipGraphExec_t graph = nullptr;
+    bool own_stream = true;
     double tab_host[NTAB * TS];
 };
 
@@ -733,7 +734,84 @@ gqmap_status download(gqmap_ctx *c, double *dst, const void *src, size_t n)
     return GQMAP_OK;
 }
 
+
+// Shape checks and (re)allocation for a Mo x No frame pair; VV storage type
+// vv32 (float) or double.  Invalidates the state when the grid changes.
+gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
+{
+    GQ_CHECK(Mo >= 4 && No >= 4, GQMAP_ERR_INVALID_ARG, "image %dx%d too small", Mo, No);
+    if (c->super_)
+        GQ_CHECK(Mo % 4 == 0 && No % 4 == 0, GQMAP_ERR_INVALID_ARG,
+                 "super engine needs Mo,No divisible by 4 (got %dx%d)", Mo, No);
+    const int M = c->super_ ? Mo / 4 : Mo, N = c->super_ ? No / 4 : No;
+    GQ_CHECK(M >= 3 && N >= 3, GQMAP_ERR_INVALID_ARG, "node grid %dx%d has no interior", M, N);
+    DeviceGuard dg(c->device);
+    const bool resize = Mo != c->Mo || No != c->No || vv32 != c->vv32 || !c->d_VV;
+    c->Mo = Mo;
+    c->No = No;
+    c->M = M;
+    c->N = N;
+    c->MNL = (int64_t)c->M * c->N * c->L;
+    c->vv32 = vv32;
+    if (resize) {
+        drop_graph(c);
+        if (c->d_VV) (void)hipFree(c->d_VV);
+        if (c->d_I1) (void)hipFree(c->d_I1);
+        c->d_VV = c->d_I1 = nullptr;
+        GQ_HIP(hipMalloc(&c->d_VV, (size_t)(Mo + 2) * (No + 2) * (vv32 ? sizeof(float) : sizeof(double))));
+        GQ_HIP(hipMalloc(&c->d_I1, (size_t)Mo * No * c->rsz));
+        gqmap_status s = alloc_grid(c);
+        if (s != GQMAP_OK) return s;
+        c->have_state = false;
+    }
+    return GQMAP_OK;
+}
+
 }  // namespace
+
+// ---- internal API for the coarse-to-fine driver (gqmap_pyramid.hip) -------
+namespace gq {
+
+gqmap_status ctx_set_images_device(gqmap_ctx *c, const double *dI1, const double *dI2, int Mo, int No,
+                                   double *d_scratch, int *d_flag)
+{
+    // getVV on the device into d_scratch ((Mo+2)*(No+2) doubles), then the
+    // same float-exactness policy as gqmap_set_images
+    DeviceGuard dg(c->device);
+    GQ_HIP(pad_vv_device(dI2, Mo, No, d_scratch, c->stream));
+    const size_t nvv = (size_t)(Mo + 2) * (No + 2);
+    bool vv32 = c->fp32;
+    if (!vv32 && !std::getenv("GQMAP_VV64")) GQ_HIP(f32_exact_device(d_scratch, nvv, d_flag, &vv32, c->stream));
+    gqmap_status s = prepare_images(c, Mo, No, vv32);
+    if (s != GQMAP_OK) return s;
+    GQ_HIP(convert_device(d_scratch, c->d_VV, nvv, vv32, c->stream));
+    GQ_HIP(convert_device(dI1, c->d_I1, (size_t)Mo * No, c->fp32, c->stream));
+    c->have_images = true;
+    return GQMAP_OK;
+}
+
+gqmap_status ctx_flow_device(gqmap_ctx *c, const void **muu, const void **muv, bool *fp32)
+{
+    Ctl h;
+    gqmap_status s = read_ctl(c, &h);
+    if (s != GQMAP_OK) return s;
+    const char *cur = (const char *)c->d_st[h.done & 1];
+    *muu = cur;
+    *muv = cur + (size_t)c->MNL * c->rsz;
+    *fp32 = c->fp32;
+    return GQMAP_OK;
+}
+
+void ctx_adopt_stream(gqmap_ctx *c, hipStream_t s)
+{
+    DeviceGuard dg(c->device);
+    drop_graph(c);
+    if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
+    c->stream = s;
+    c->own_stream = false;
+}
+
+}  // namespace gq
 
 extern "C" {
 
@@ -865,21 +943,8 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
 {
     clear_error();
     GQ_CHECK(c && I1 && I2, GQMAP_ERR_INVALID_ARG, "gqmap_set_images: null argument");
-    GQ_CHECK(Mo >= 4 && No >= 4, GQMAP_ERR_INVALID_ARG, "image %dx%d too small", Mo, No);
-    if (c->super_)
-        GQ_CHECK(Mo % 4 == 0 && No % 4 == 0, GQMAP_ERR_INVALID_ARG,
-                 "super engine needs Mo,No divisible by 4 (got %dx%d)", Mo, No);
-    DeviceGuard dg(c->device);
-    bool resize = Mo != c->Mo || No != c->No;
-    c->Mo = Mo;
-    c->No = No;
-    c->M = c->super_ ? Mo / 4 : Mo;
-    c->N = c->super_ ? No / 4 : No;
-    GQ_CHECK(c->M >= 3 && c->N >= 3, GQMAP_ERR_INVALID_ARG, "node grid %dx%d has no interior",
-             c->M, c->N);
-    c->MNL = (int64_t)c->M * c->N * c->L;
     std::vector<double> VV((size_t)(Mo + 2) * (No + 2));
-    build_padded(I2, Mo, No, VV.data());
+    if (Mo >= 4 && No >= 4) build_padded(I2, Mo, No, VV.data());
     // fp64 engine: keep the padded image in float when that is exact (frames
     // from rgb2gray are integers; their cubic padding stays in [-510, 765]):
     // same values, half the gather bytes.
@@ -889,21 +954,9 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
         for (double v : VV)
             if ((double)(float)v != v) { vv32 = false; break; }
     }
-    if (vv32 != c->vv32) resize = true;
-    c->vv32 = vv32;
-    const size_t vsz = vv32 ? sizeof(float) : sizeof(double);
-    if (resize || !c->d_VV) {
-        drop_graph(c);
-        if (c->d_VV) (void)hipFree(c->d_VV);
-        if (c->d_I1) (void)hipFree(c->d_I1);
-        c->d_VV = c->d_I1 = nullptr;
-        GQ_HIP(hipMalloc(&c->d_VV, VV.size() * vsz));
-        GQ_HIP(hipMalloc(&c->d_I1, (size_t)Mo * No * c->rsz));
-        gqmap_status s = alloc_grid(c);
-        if (s != GQMAP_OK) return s;
-        c->have_state = false;
-    }
-    gqmap_status s;
+    gqmap_status s = prepare_images(c, Mo, No, vv32);
+    if (s != GQMAP_OK) return s;
+    DeviceGuard dg(c->device);
     if (vv32) {
         std::vector<float> v32(VV.begin(), VV.end());
         GQ_HIP(hipMemcpy(c->d_VV, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -1210,7 +1263,7 @@ void gqmap_destroy(gqmap_ctx *c)
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 

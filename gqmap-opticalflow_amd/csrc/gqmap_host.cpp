@@ -48,6 +48,64 @@ void build_padded(const double *I2, int M, int N, double *VV)
     }
 }
 
+// imresize 'bicubic' kernel (Keys, a = -0.5) in its unscaled form
+static double keys_cubic(double x)
+{
+    const double ax = std::fabs(x), ax2 = ax * ax, ax3 = ax2 * ax;
+    return ax <= 1.0 ? 1.5 * ax3 - 2.5 * ax2 + 1.0
+         : ax <= 2.0 ? -0.5 * ax3 + 2.5 * ax2 - 4.0 * ax + 2.0
+                     : 0.0;
+}
+
+int resize_len(int len, double scale) { return (int)std::ceil(scale * (double)len); }
+
+// MATLAB imresize contributions(): output sample x (1-based) sits at
+// u = x/scale + (1 - 1/scale)/2 in input coordinates; taps left..left+P-1
+// with left = floor(u - width/2); a reduction widens the kernel to 4/scale
+// and scales it by `scale` (antialiasing); rows are normalised to sum 1;
+// out-of-range taps mirror symmetrically; tap columns that are zero for
+// every output are dropped (so scale 1 is an exact copy).
+int resize_contrib(int in_len, int out_len, double scale, int antialias, std::vector<double> &w,
+                   std::vector<int> &idx)
+{
+    const bool aa = antialias && scale < 1.0;
+    const double width = aa ? 4.0 / scale : 4.0;
+    const int P = (int)std::ceil(width) + 2;
+    std::vector<double> wf((size_t)out_len * P);
+    std::vector<int> jf((size_t)out_len * P);
+    const long period = 2L * in_len;
+    for (int i = 0; i < out_len; ++i) {
+        const double u = (double)(i + 1) / scale + 0.5 * (1.0 - 1.0 / scale);
+        const double left = std::floor(u - width / 2.0);
+        double *wr = &wf[(size_t)i * P];
+        double sum = 0.0;
+        for (int k = 0; k < P; ++k) {
+            const double d = u - (left + (double)k);
+            wr[k] = aa ? scale * keys_cubic(scale * d) : keys_cubic(d);
+            sum += wr[k];
+        }
+        for (int k = 0; k < P; ++k) {
+            wr[k] /= sum;
+            long j = ((long)left + k - 1) % period;
+            if (j < 0) j += period;
+            jf[(size_t)i * P + k] = (int)(j < in_len ? j : period - 1 - j);
+        }
+    }
+    std::vector<int> keep;
+    for (int k = 0; k < P; ++k)
+        for (int i = 0; i < out_len; ++i)
+            if (wf[(size_t)i * P + k] != 0.0) { keep.push_back(k); break; }
+    const int Pk = (int)keep.size();
+    w.assign((size_t)out_len * Pk, 0.0);
+    idx.assign((size_t)out_len * Pk, 0);
+    for (int i = 0; i < out_len; ++i)
+        for (int k = 0; k < Pk; ++k) {
+            w[(size_t)i * Pk + k] = wf[(size_t)i * P + keep[k]];
+            idx[(size_t)i * Pk + k] = jf[(size_t)i * P + keep[k]];
+        }
+    return Pk;
+}
+
 // Gauss-Hermite nodes/weights for int exp(-x^2) f(x): Newton iteration on the
 // orthonormal Hermite recurrence with asymptotic starting guesses.  The
 // reference (GaussHermite_2.m) takes the eigen-decomposition of the Jacobi

@@ -5,6 +5,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <vector>
 
 #include "../../include/gqmap.h"
 
@@ -66,4 +67,32 @@ void build_padded(const double *I2, int M, int N, double *VV);
 // Gauss-Hermite by Newton iteration on the orthonormal Hermite recurrence.
 int gauss_hermite(int K, double *x, double *w);
 
+// ---- coarse-to-fine plumbing (legacy/optical_flow_ctf.m:21-35) -------------
+// MATLAB imresize contributions(): Keys kernel widened by 1/scale when
+// antialiasing a reduction, symmetric edge mirroring, all-zero tap columns
+// removed.  w/idx: [out_len][P] row-major, idx 0-based; returns P.
+int resize_contrib(int in_len, int out_len, double scale, int antialias, std::vector<double> &w,
+                   std::vector<int> &idx);
+// imresize output length: ceil(scale * len)
+int resize_len(int len, double scale);
+
+// device helpers (gqmap_pyramid.hip), all asynchronous on s unless noted
+hipError_t pad_vv_device(const double *dI2, int M, int N, double *dVV, hipStream_t s);
+// *exact = every value representable in float (synchronises s)
+hipError_t f32_exact_device(const double *d, size_t n, int *d_flag, bool *exact, hipStream_t s);
+hipError_t convert_device(const double *src, void *dst, size_t n, bool to_f32, hipStream_t s);
+
+}  // namespace gq
+
+// ---- engine context, internal API used by the coarse-to-fine driver -------
+struct gqmap_ctx;
+namespace gq {
+// images already on the device (fp64 M x N each); d_scratch holds
+// (Mo+2)*(No+2) doubles, d_flag one int
+gqmap_status ctx_set_images_device(gqmap_ctx *c, const double *dI1, const double *dI2, int Mo, int No,
+                                   double *d_scratch, int *d_flag);
+// current muu / muv planes (fp64 or fp32 per *fp32); synchronises the stream
+gqmap_status ctx_flow_device(gqmap_ctx *c, const void **muu, const void **muv, bool *fp32);
+// run the context on a caller-owned stream
+void ctx_adopt_stream(gqmap_ctx *c, hipStream_t s);
 }  // namespace gq

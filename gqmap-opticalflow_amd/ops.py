@@ -4,6 +4,8 @@ flow_to_color   flowToColor_mex (legacy/flowToColor.m:37-87 + legacy/computeColo
 mixture_map     get_map_mex     (legacy/findMixMax.m:39-70 semantics, fminbnd TolX 1e-4)
 projsplx        projsplx.m:15-30, batched over columns (projsplx.m:34-67)
 gauss_hermite   GaussHermite_2.m (host)
+imresize        imresize(A, scale) bicubic + antialias (legacy/optical_flow_ctf.m:26-29)
+warp_image      interp2 linear + fillmissing nearest (legacy/optical_flow_ctf.m:30-32)
 """
 from __future__ import annotations
 
@@ -59,3 +61,34 @@ def gauss_hermite(K: int):
     x, w = np.zeros(K), np.zeros(K)
     check(_lib.load().gqmap_gauss_hermite(K, dptr(x), dptr(w)), "gqmap_gauss_hermite")
     return x, w
+
+
+def resize_len(n: int, scale: float) -> int:
+    """imresize output length ceil(scale * n)."""
+    return int(_lib.load().gqmap_resize_len(int(n), float(scale)))
+
+
+def imresize(A, scale: float, antialias: bool = True, device: int = 0) -> np.ndarray:
+    """imresize(A, scale) with MATLAB's defaults ('bicubic', Antialiasing on
+    when shrinking) for an M x N (x C) double array, resampled on the device."""
+    A = f64(A)
+    M, N = A.shape[:2]
+    Cn = 1 if A.ndim == 2 else int(np.prod(A.shape[2:]))
+    oM, oN = resize_len(M, scale), resize_len(N, scale)
+    out = np.zeros((oM, oN) + A.shape[2:], order="F")
+    check(_lib.load().gqmap_imresize(dptr(A), M, N, Cn, float(scale), int(antialias), dptr(out),
+                                     device), "gqmap_imresize")
+    return out
+
+
+def warp_image(V, warp, fill: bool = True, device: int = 0) -> np.ndarray:
+    """interp2(V, x - warp(:,:,1), y - warp(:,:,2)) (linear, NaN outside),
+    then fillmissing(.,'nearest',1) and (.,'nearest',2) when fill."""
+    V, warp = f64(V), f64(warp)
+    M, N = V.shape
+    if warp.shape != (M, N, 2):
+        raise ValueError(f"warp must be {M}x{N}x2, got {warp.shape}")
+    out = np.zeros((M, N), order="F")
+    check(_lib.load().gqmap_warp_image(dptr(V), M, N, dptr(warp), int(fill), dptr(out), device),
+          "gqmap_warp_image")
+    return out

@@ -155,7 +155,48 @@ gqmap_status gqmap_flow_to_color(const double *flow, int M, int N, double max_fl
                                  uint8_t *img, double *flo, double *stats, uint8_t *unknown,
                                  int device);
 
+/* imresize(A, scale) (MATLAB default 'bicubic', Antialiasing on for scale<1)
+ * of an M x N x C array -> ceil(scale*M) x ceil(scale*N) x C, resampled on the
+ * device (legacy/optical_flow_ctf.m:26-27, 29). */
+gqmap_status gqmap_imresize(const double *in, int M, int N, int C, double scale, int antialias,
+                            double *out, int device);
+/* interp2(V, x - warp(:,:,1), y - warp(:,:,2)) bilinear, NaN outside
+ * (optical_flow_ctf.m:30-31); fill != 0 then applies fillmissing 'nearest'
+ * along dim 1 and then dim 2 (:32).  V M x N, warp M x N x 2. */
+gqmap_status gqmap_warp_image(const double *V, int M, int N, const double *warp, int fill,
+                              double *out, int device);
+
+/* ---- coarse-to-fine driver: legacy/optical_flow_ctf.m:21-35 ---- */
+#define GQMAP_CTF_MAX_LEVELS 8
+typedef struct gqmap_pyramid gqmap_pyramid;
+/* level_opt: options of every level (engine GQMAP_ENGINE_CTF, its = iterations
+ * per level); minu..maxv = range of the FULL-RESOLUTION ground truth: level s
+ * uses them times s, as gqmap_ctf(options,I1_w,I2,trueFlow.*scale) does
+ * (optical_flow_ctf.m:33, gqmap_ctf.m:4).  scales: n_levels ascending factors,
+ * e.g. {1/16,1/8,1/4,1/2,1}; each level must be exactly twice the previous. */
+gqmap_status gqmap_ctf_create(gqmap_pyramid **out, const gqmap_options *level_opt,
+                              const double *scales, int n_levels, int device);
+/* Full-resolution frames img1/img2 (M x N double): each level's frames are
+ * resampled on the device (imresize, :26-27). */
+gqmap_status gqmap_ctf_set_images(gqmap_pyramid *p, const double *img1, const double *img2, int M,
+                                  int N);
+/* The whole pyramid on the device: per level prolong (imresize(warp,2).*2,
+ * :29), warp I1 (interp2 + fillmissing, :30-32), seeded init (seed + level),
+ * the level solver (gqmap_ctf) and warp += flow (:34).  flow: M x N x 2 final
+ * warp; its_done[n_levels]; elapsed_ms: wall time of the pyramid (all may be
+ * NULL). */
+gqmap_status gqmap_ctf_run(gqmap_pyramid *p, uint64_t seed, double *flow, int *its_done,
+                           double *elapsed_ms);
+/* Intermediates of level `level` after a run (each output may be NULL): the
+ * warped I1 and resampled I2 (Ml x Nl), the level's flow and the warp after
+ * the level (Ml x Nl x 2). */
+gqmap_status gqmap_ctf_get_level(gqmap_pyramid *p, int level, int *Ml, int *Nl, double *I1w,
+                                 double *I2, double *flow, double *warp);
+void gqmap_ctf_destroy(gqmap_pyramid *p);
+
 /* ---- host helpers (no device needed) ---- */
+/* imresize output length for a scale factor: ceil(scale*len). */
+int gqmap_resize_len(int len, double scale);
 /* GaussHermite_2(K) (GaussHermite_2.m): nodes ascending + weights. */
 gqmap_status gqmap_gauss_hermite(int K, double *x, double *w);
 /* U(0,1) doubles of stream `stream`, indices [first, first+n): the RNG used by

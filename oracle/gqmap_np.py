@@ -336,3 +336,102 @@ def flow_to_color(flow, max_flow=0.0):
         img[:, :, i] = np.clip(np.floor(255 * col * (1 - nan)), 0, 255).astype(np.uint8)
     img[unk] = 0
     return img, flo, (minu, maxu, minv, maxv), unk
+
+
+# ---- coarse-to-fine plumbing (legacy/optical_flow_ctf.m:21-35), vectorised ----
+# Independent of oracle/gqmap_pyramid_oracle.c: MATLAB-style whole-array
+# expressions (numpy sums and powers), bilinear sampling by
+# scipy.ndimage.map_coordinates.  Agreement with the C restatement is to
+# rounding (~1e-13), not bitwise.
+def _cubic_np(x):
+    ax = np.abs(x)
+    ax2, ax3 = ax ** 2, ax ** 3
+    return ((1.5 * ax3 - 2.5 * ax2 + 1) * (ax <= 1)
+            + (-0.5 * ax3 + 2.5 * ax2 - 4 * ax + 2) * ((1 < ax) & (ax <= 2)))
+
+
+def imresize_contrib(in_len, out_len, scale, antialias=True):
+    """imresize.m contributions(): (weights [out,P], 0-based indices [out,P])."""
+    if scale < 1 and antialias:
+        h = lambda x: scale * _cubic_np(scale * x)
+        width = 4.0 / scale
+    else:
+        h, width = _cubic_np, 4.0
+    x = np.arange(1, out_len + 1, dtype=np.float64)[:, None]
+    u = x / scale + 0.5 * (1 - 1 / scale)
+    left = np.floor(u - width / 2)
+    P = int(np.ceil(width)) + 2
+    ind = left + np.arange(P)[None, :]
+    w = h(u - ind)
+    w = w / w.sum(axis=1, keepdims=True)
+    aux = np.concatenate([np.arange(1, in_len + 1), np.arange(in_len, 0, -1)])
+    ind = aux[np.mod(ind - 1, aux.size).astype(np.int64)]
+    keep = np.any(w != 0, axis=0)
+    return w[:, keep], ind[:, keep] - 1
+
+
+def imresize(A, scale, antialias=True):
+    A = np.asarray(A, dtype=np.float64)
+    M, N = A.shape[:2]
+    oM, oN = int(np.ceil(scale * M)), int(np.ceil(scale * N))
+    wm, im = imresize_contrib(M, oM, scale, antialias)
+    wn, jn = imresize_contrib(N, oN, scale, antialias)
+    B = np.einsum("ik,ik...->i...", wm, A[im])                 # dim 1
+    B = np.einsum("jk,ijk...->ij...", wn, B[:, jn])            # dim 2
+    return np.asfortranarray(B)
+
+
+def warp_image(V, warp, fill=True):
+    from scipy.ndimage import map_coordinates
+    V = np.asarray(V, dtype=np.float64)
+    M, N = V.shape
+    xs, ys = np.meshgrid(np.arange(1, N + 1), np.arange(1, M + 1))
+    xq, yq = xs - warp[:, :, 0], ys - warp[:, :, 1]
+    out = map_coordinates(V, [yq - 1, xq - 1], order=1, mode="constant", cval=np.nan)
+    out[~((xq >= 1) & (xq <= N) & (yq >= 1) & (yq <= M))] = np.nan
+    out = np.asfortranarray(out)
+    if fill:
+        out = fillmissing_nearest(fillmissing_nearest(out, 1), 2)
+    return out
+
+
+def fillmissing_nearest(A, dim):
+    A = np.array(A, dtype=np.float64, order="F")
+    B = A if dim == 1 else A.T
+    for c in range(B.shape[1]):
+        col = B[:, c]
+        ok = np.flatnonzero(~np.isnan(col))
+        bad = np.flatnonzero(np.isnan(col))
+        if ok.size == 0 or bad.size == 0:
+            continue
+        pos = np.searchsorted(ok, bad)               # next valid at ok[pos]
+        nxt = ok[np.minimum(pos, ok.size - 1)]
+        prv = ok[np.maximum(pos - 1, 0)]
+        use_prev = (pos == ok.size) | ((pos > 0) & (bad - prv < nxt - bad))
+        col[bad] = np.where(use_prev, col[prv], col[nxt])
+    return np.asfortranarray(A)
+
+
+def ctf_pipeline(opts, img1, img2, scales, init_fn):
+    """optical_flow_ctf.m:21-35 with this module's Engine("ctf") as the level solver."""
+    M, N = img1.shape
+    s0 = scales[0]
+    warp = np.zeros((int(np.ceil(M * s0 / 2)), int(np.ceil(N * s0 / 2)), 2))
+    levels = []
+    for l, s in enumerate(scales):
+        I1, I2 = imresize(img1, s), imresize(img2, s)
+        warp = imresize(warp, 2.0) * 2
+        I1w = warp_image(I1, warp)
+        lo = dict(opts, engine="ctf", minu=opts["minu"] * s, maxu=opts["maxu"] * s,
+                  minv=opts["minv"] * s, maxv=opts["maxv"] * s)
+        st = init_fn(l, lo, *I1.shape)
+        eng = Engine(lo, I1w, I2)
+        T = 0.0
+        for it in range(1, int(lo["its"]) + 1):
+            e, ptdmu, _ = eng.iterate(st, it, T)[:3]
+            if ptdmu < lo.get("tor", 1e-4):
+                break
+        flow = np.stack([st["muu"][:, :, 0], st["muv"][:, :, 0]], axis=2)
+        warp = warp + flow
+        levels.append(dict(I1w=I1w, I2=I2, flow=flow, warp=warp.copy()))
+    return warp, levels

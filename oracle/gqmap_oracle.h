@@ -88,6 +88,18 @@ void orc_get_map(const double *alpha, const double *muu, const double *sigu,
                  const double *muv, const double *sigv, int M, int N, int L,
                  double *out, int nthreads);
 
+/* ---- coarse-to-fine plumbing (gqmap_pyramid_oracle.c) ----------------- */
+/* imresize.m contributions(): taps before/after removing all-zero columns */
+int orc_resize_taps(double scale, int antialias);
+int orc_resize_contrib(int in_len, int out_len, double scale, int antialias, double *w, int *idx);
+int orc_resize_len(int len, double scale);
+/* imresize(A, scale) bicubic (+antialias for scale<1), A M x N x C */
+void orc_imresize(const double *in, int M, int N, int C, double scale, int antialias, double *out);
+/* interp2(V, x-warp(:,:,1), y-warp(:,:,2)) linear, NaN outside */
+void orc_warp_image(const double *V, int M, int N, const double *warp, double *out);
+/* fillmissing(A,'nearest',dim) in place */
+void orc_fillmissing_nearest(double *A, int M, int N, int dim);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,7 +40,8 @@ class OrcState(C.Structure):
 
 def build() -> str:
     path = os.path.join(_HERE, "liboracle.so")
-    srcs = [os.path.join(_HERE, f) for f in ("gqmap_oracle.c", "gqmap_oracle.h", "gqmap_emul.cpp")]
+    srcs = [os.path.join(_HERE, f) for f in ("gqmap_oracle.c", "gqmap_oracle.h", "gqmap_emul.cpp",
+                                             "gqmap_pyramid_oracle.c", "Makefile")]
     srcs.append(os.path.join(os.path.dirname(_HERE), "gqmap-opticalflow_amd", "csrc", "gqmap_math.h"))
     if not os.path.exists(path) or os.path.getmtime(path) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE])
@@ -252,3 +253,96 @@ def emu_math(fn: int, x) -> np.ndarray:
     f.argtypes = [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int64]
     f(fn, _p(x), _p(out), x.size)
     return out
+
+
+# ---- coarse-to-fine plumbing (gqmap_pyramid_oracle.c) -----------------------
+def resize_len(n: int, scale: float) -> int:
+    f = lib().orc_resize_len
+    f.restype = C.c_int
+    f.argtypes = [C.c_int, C.c_double]
+    return f(int(n), float(scale))
+
+
+def imresize(A, scale: float, antialias: bool = True) -> np.ndarray:
+    """imresize(A, scale) restated (bicubic, antialias when shrinking)."""
+    A = _f64(np.asarray(A, dtype=np.float64))
+    M, N = A.shape[:2]
+    Cn = 1 if A.ndim == 2 else int(np.prod(A.shape[2:]))
+    out = np.zeros((resize_len(M, scale), resize_len(N, scale)) + A.shape[2:], order="F")
+    f = lib().orc_imresize
+    f.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int, C.c_double, C.c_int,
+                  C.POINTER(C.c_double)]
+    f(_p(A), M, N, Cn, float(scale), int(antialias), _p(out))
+    return out
+
+
+def resize_contrib(in_len: int, out_len: int, scale: float, antialias: bool = True):
+    P = lib().orc_resize_taps
+    P.restype = C.c_int
+    P.argtypes = [C.c_double, C.c_int]
+    p = P(float(scale), int(antialias))
+    w = np.zeros(out_len * p)
+    idx = np.zeros(out_len * p, dtype=np.int32)
+    f = lib().orc_resize_contrib
+    f.restype = C.c_int
+    f.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+    k = f(in_len, out_len, float(scale), int(antialias), _p(w), idx.ctypes.data_as(C.POINTER(C.c_int)))
+    return w[:out_len * k].reshape(out_len, k), idx[:out_len * k].reshape(out_len, k)
+
+
+def warp_image(V, warp, fill: bool = True) -> np.ndarray:
+    """interp2 linear warp (+ fillmissing nearest dim 1 then 2)."""
+    V, warp = _f64(V), _f64(warp)
+    M, N = V.shape
+    out = np.zeros((M, N), order="F")
+    f = lib().orc_warp_image
+    f.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    f(_p(V), M, N, _p(warp), _p(out))
+    if fill:
+        fillmissing_nearest(out, 1)
+        fillmissing_nearest(out, 2)
+    return out
+
+
+def fillmissing_nearest(A: np.ndarray, dim: int) -> np.ndarray:
+    """In place on a Fortran-ordered float64 array (returned for chaining)."""
+    assert A.flags.f_contiguous and A.dtype == np.float64
+    M, N = A.shape
+    f = lib().orc_fillmissing_nearest
+    f.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int]
+    f(_p(A), M, N, int(dim))
+    return A
+
+
+def ctf_pipeline(opts: dict, img1, img2, scales, init_fn, *, solver: str = "emu", X=None, W=None,
+                 nthreads: int = 0, fp32: bool = False):
+    """legacy/optical_flow_ctf.m:21-35 with the restated plumbing.
+
+    opts: level options (engine "ctf", its per level) with the FULL-RES GT
+    range minu..maxv; level s uses it times s (gqmap_ctf.m:4 on trueFlow.*scale).
+    init_fn(level, level_opts, M, N) -> State for the level (the caller's
+    seeded initialisation).  solver "emu" (CPU model of the kernel, needs
+    X, W) or "literal" (gqmap_oracle.c).  Returns (final warp, per-level dicts)."""
+    img1, img2 = _f64(img1), _f64(img2)
+    M, N = img1.shape
+    s0 = scales[0]
+    warp = np.zeros((resize_len(M, s0 / 2), resize_len(N, s0 / 2), 2), order="F")
+    levels = []
+    for l, s in enumerate(scales):
+        I1 = imresize(img1, s)
+        I2 = imresize(img2, s)
+        warp = _f64(imresize(warp, 2.0) * 2)
+        I1w = warp_image(I1, warp)
+        lo = dict(opts, engine="ctf", minu=opts["minu"] * s, maxu=opts["maxu"] * s,
+                  minv=opts["minv"] * s, maxv=opts["maxv"] * s)
+        Ml, Nl = I1.shape
+        st = init_fn(l, lo, Ml, Nl)
+        its = int(lo["its"])
+        if solver == "emu":
+            done, tr, _ = emu_run(lo, I1w, I2, st, 1, its, X, W, nthreads=nthreads, fp32=fp32)
+        else:
+            done, tr, _ = run(lo, I1w, I2, st, 1, its, nthreads=nthreads)
+        flow = np.stack([st.muu[:, :, 0], st.muv[:, :, 0]], axis=2)
+        warp = _f64(warp + flow)
+        levels.append(dict(I1w=I1w, I2=I2, flow=flow, warp=warp.copy(), its=done, trace=tr))
+    return warp, levels

@@ -110,7 +110,49 @@ def make_color():
     print("flow_to_color", img.shape, stats)
 
 
+# coarse-to-fine driver (legacy/optical_flow_ctf.m:21-35) on a Grove3 crop:
+# 3 levels 16x24 -> 32x48 -> 64x96, a few iterations per level, explicit
+# per-level initial states (sigma = U + 3, gqmap_ctf.m:16-17)
+CTF_PIPE = dict(crop=(150, 200, 64, 96), scales=(0.25, 0.5, 1.0), its=4, K=11, seed=50)
+
+
+def ctf_level_state(seed, l, M, N, lo):
+    rng = np.random.default_rng(seed + l)
+    du, dv = lo["maxu"] - lo["minu"], lo["maxv"] - lo["minv"]
+    f = lambda a: np.asfortranarray(a.reshape(M, N, 1))
+    return dict(muu=f(lo["minu"] + rng.random(M * N) * du), muv=f(lo["minv"] + rng.random(M * N) * dv),
+                sigu=f(rng.random(M * N) + 3), sigv=f(rng.random(M * N) + 3),
+                pn=np.zeros((M, N, 1), order="F"), rou=np.zeros((M, N, 1, 2, 2), order="F"),
+                w=np.zeros(1), alpha=np.ones(1))
+
+
+def make_ctf_pipeline():
+    c = CTF_PIPE
+    r0, c0, M, N = c["crop"]
+    img1, img2, gt = crop_pair(r0, c0, M, N, "Grove3")
+    _, _, (minu, maxu, minv, maxv), _ = gqmap_np.flow_to_color(gt)
+    opts = dict(engine="ctf", K=c["K"], L=1, its=c["its"], epsn=1e-6, lambdas=5.0, lambdad=1.0,
+                temperature=0.0, minu=float(minu), maxu=float(maxu), minv=float(minv), maxv=float(maxv))
+    inits = {}
+
+    def init_fn(l, lo, Ml, Nl):
+        st = ctf_level_state(c["seed"], l, Ml, Nl, lo)
+        inits[l] = {k: v.copy() for k, v in st.items()}
+        return st
+
+    warp, levels = gqmap_np.ctf_pipeline(opts, img1, img2, c["scales"], init_fn)
+    out = dict(img1=img1, img2=img2, scales=np.array(c["scales"]), warp=warp)
+    for l, lv in enumerate(levels):
+        for k, v in lv.items():
+            out[f"L{l}_{k}"] = v
+        for k, v in inits[l].items():
+            out[f"L{l}_init_{k}"] = v
+    np.savez_compressed(os.path.join(HERE, "ctf_pipeline.npz"), opts=np.array(repr(opts)), **out)
+    print("ctf_pipeline", [lv["I1w"].shape for lv in levels], float(np.abs(warp).max()))
+
+
 if __name__ == "__main__":
     for n, c in CASES.items():
         make_case(n, c)
     make_color()
+    make_ctf_pipeline()
