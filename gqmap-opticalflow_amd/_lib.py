@@ -28,7 +28,8 @@ EXPORTS = (
     "gqmap_mixture_map", "gqmap_flow_to_color", "gqmap_gauss_hermite", "gqmap_rand_uniform",
     "gqmap_last_error", "gqmap_abi_version", "gqmap_device_count", "gqmap_imresize",
     "gqmap_warp_image", "gqmap_ctf_create", "gqmap_ctf_set_images", "gqmap_ctf_run",
-    "gqmap_ctf_get_level", "gqmap_ctf_destroy", "gqmap_resize_len",
+    "gqmap_ctf_get_level", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
+    "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run",
 )
 CTF_MAX_LEVELS = 8
 
@@ -59,7 +60,8 @@ class GqmapState(C.Structure):
 class GqmapInfo(C.Structure):
     _fields_ = [("Mo", C.c_int), ("No", C.c_int), ("M", C.c_int), ("N", C.c_int),
                 ("L", C.c_int), ("K", C.c_int), ("it", C.c_int), ("stopped", C.c_int),
-                ("T", C.c_double), ("device", C.c_int), ("split", C.c_int)]
+                ("T", C.c_double), ("device", C.c_int), ("split", C.c_int),
+                ("n_tiles", C.c_int), ("tile", C.c_int), ("col0", C.c_int), ("col1", C.c_int)]
 
 
 class GqmapError(RuntimeError):
@@ -111,6 +113,10 @@ def load():
         "gqmap_ctf_get_level": (C.c_int, [vp, C.c_int, P(C.c_int), P(C.c_int), _D, _D, _D, _D]),
         "gqmap_ctf_destroy": (None, [vp]),
         "gqmap_resize_len": (C.c_int, [C.c_int, C.c_double]),
+        "gqmap_create_tile": (C.c_int, [P(vp), P(GqmapOptions), C.c_int, C.c_int, C.c_int]),
+        "gqmap_comm_unique_id": (C.c_int, [u8]),
+        "gqmap_tile_attach_rccl": (C.c_int, [vp, u8]),
+        "gqmap_tile_group_run": (C.c_int, [P(vp), C.c_int, C.c_int, P(C.c_int), _D]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

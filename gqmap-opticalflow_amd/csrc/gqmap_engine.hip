@@ -23,7 +23,9 @@
 // rou(dir=2,u), rou(dir=1,v), rou(dir=2,v) -- i.e. rou(m,n,l,dir,uv) exactly as
 // the reference's 5-D array.  Tiles of 16x16 nodes map to 256-thread
 // workgroups (4 wave64s); lane order is m-fastest so state loads coalesce.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -105,6 +107,11 @@ struct IterParams {
     Ctl *ctl;
     fix128 *partials;           // nblocks x (NFIX + L)
     int M, N, Mo, No, M2, L, K2;
+    // column-strip tiling (multi-GPU): local node column n is global column
+    // n + n_off of Ng; only local columns [own_lo, own_hi) are updated, the
+    // others are ghost copies of the neighbours' boundary columns.  A single
+    // context has n_off = 0, [0, N), Ng = N.
+    int n_off, own_lo, own_hi, Ng;
     int tiles_m, tiles_n;
     R epsn, lamd, lams;
     R minu, maxu, minv, maxv, sig_lo, sig_hi, corr, sig_step;
@@ -203,7 +210,10 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     const int M = P.M, N = P.N;
     const int64_t MNL = P.MNL, MN = (int64_t)M * N;
     const bool valid = m < M && n < N;
-    auto interior = [&](int mm, int nn) { return mm >= 1 && mm <= M - 2 && nn >= 1 && nn <= N - 2; };
+    auto interior = [&](int mm, int nn) {
+        return mm >= 1 && mm <= M - 2 && nn >= P.own_lo && nn < P.own_hi && nn + P.n_off >= 1 &&
+               nn + P.n_off <= P.Ng - 2;
+    };
     const bool inner = valid && interior(m, n);
     const bool lead = kj == 0;  // the lane that owns the node's outputs
     const ctab_t<R> tab = as_const(P.tab);
@@ -235,7 +245,7 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
 #endif
             const NodeCoef<R> c = node_coef(own[2], own[3], own[4]);
             Sums<R> S = node_sums<ENG>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
-                                       own[0], own[1], m, n);
+                                       own[0], own[1], m, n + P.n_off);
             if (Q > 1) S = lane_combine<Q>(S);
             nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, own[2], own[3], own[4], ENG == 2);
         }
@@ -359,6 +369,8 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
 struct FinParams {
     const fix128 *partials;
     int nblocks, L;
+    const fix128 *gathered;  // nranks > 0: per-tile totals [nranks][NFIX+L] (exact, any order)
+    int nranks;
     Ctl *ctl;
     double *trace;     // TRACE_CAP x 3
     double count;      // interior nodes * L
@@ -379,7 +391,10 @@ __global__ __launch_bounds__(256) void k_finalize(FinParams F)
     const int tid = threadIdx.x;
     for (int q = 0; q < NP; ++q) {
         fix128 v = 0;
-        for (int b = tid; b < F.nblocks; b += 256) v += F.partials[(int64_t)b * NP + q];
+        if (F.nranks > 0)
+            for (int r = tid; r < F.nranks; r += 256) v += F.gathered[(int64_t)r * NP + q];
+        else
+            for (int b = tid; b < F.nblocks; b += 256) v += F.partials[(int64_t)b * NP + q];
         sh[tid] = v;
         __syncthreads();
         for (int s = 128; s > 0; s >>= 1) {
@@ -441,18 +456,66 @@ __global__ __launch_bounds__(256) void k_finalize(FinParams F)
     if (ptdmu < F.tor) ctl->stop = 1;
 }
 
+// Tiled mode: this tile's block partials -> its exact totals (one row of the
+// gathered table; the other rows arrive from the other tiles).
+__global__ __launch_bounds__(256) void k_reduce_local(const fix128 *partials, int nblocks, int NP,
+                                                      fix128 *out, const Ctl *ctl)
+{
+    if (ctl->stop) return;
+    __shared__ fix128 sh[256];
+    const int tid = threadIdx.x;
+    for (int q = 0; q < NP; ++q) {
+        fix128 v = 0;
+        for (int b = tid; b < nblocks; b += 256) v += partials[(int64_t)b * NP + q];
+        sh[tid] = v;
+        __syncthreads();
+        for (int st = 128; st > 0; st >>= 1) {
+            if (tid < st) sh[tid] += sh[tid + st];
+            __syncthreads();
+        }
+        if (tid == 0) out[q] = sh[0];
+        __syncthreads();
+    }
+}
+
+// Ghost-column exchange: the column k_iter just wrote (the ping-pong
+// destination, chosen by the device-side parity) <-> a contiguous buffer of
+// NPLANES x L x M values.  Column-major planes make each (plane, component)
+// column one contiguous run of M.
+template <typename R>
+__global__ void k_halo_copy(const Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL, int L, int col,
+                            R *buf, int to_buf)
+{
+    if (ctl->stop) return;
+    R *dst = (ctl->done & 1) ? st0 : st1;
+    const int64_t n = (int64_t)NPLANES * L * M;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int m = (int)(t % M);
+        const int64_t ql = t / M;  // q * L + l
+        const int q = (int)(ql / L), l = (int)(ql % L);
+        R *p = dst + (int64_t)q * MNL + (int64_t)l * MN + (int64_t)col * M + m;
+        if (to_buf) buf[t] = *p;
+        else *p = buf[t];
+    }
+}
+
 template <typename R>
 __global__ void k_init_state(R *st0, R *st1, int64_t MNL, uint64_t b1, uint64_t b2, uint64_t b3,
                              uint64_t b4, double minu, double maxu, double minv, double maxv,
-                             double sig_init)
+                             double sig_init, int M, int N, int n_off, int Ng)
 {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= MNL) return;
+    // the random streams are indexed by the GLOBAL node index, so a tile draws
+    // exactly the values the untiled grid has in its columns
+    const int64_t MN = (int64_t)M * N;
+    const int64_t l = i / MN, rem = i % MN;
+    const int64_t g = rem % M + (int64_t)M * (rem / M + n_off) + (int64_t)M * Ng * l;
     // gqmap_gpu_mixture.m:19-24 (gqmap_ctf.m:14-17: sigma = rand + 3); no
     // contraction: same bits as the host formula
     const double su = sig_init < 0 ? maxu - minu : sig_init, sv = sig_init < 0 ? maxv - minv : sig_init;
-    const R v[NPLANES] = {R(minu + u01(b1, i) * (maxu - minu)), R(minv + u01(b2, i) * (maxv - minv)),
-                          R(u01(b3, i) + su),                   R(u01(b4, i) + sv),
+    const R v[NPLANES] = {R(minu + u01(b1, g) * (maxu - minu)), R(minv + u01(b2, g) * (maxv - minv)),
+                          R(u01(b3, g) + su),                   R(u01(b4, g) + sv),
                           R(0), R(0), R(0), R(0), R(0)};
 #pragma unroll
     for (int q = 0; q < NPLANES; ++q) {
@@ -549,6 +612,18 @@ struct gqmap_ctx {
     hipGraphExec_t graph = nullptr;
     bool own_stream = true;
     double tab_host[NTAB * TS];
+    // column-strip tiling (gqmap_create_tile): node columns [col0, col1) of Ng
+    // owned, plus one ghost column per neighbour; M x N above is the LOCAL grid
+    int n_tiles = 1, tile = 0, Ng = 0, col0 = 0, col1 = 0, n_off = 0, own_lo = 0, own_hi = 0;
+    // cross-tile exchange: per-tile exact totals [nranks][NFIX+L] (nranks = 0:
+    // single context, k_finalize reduces its own partials), ghost-column
+    // send/recv buffers (left send, right send, left recv, right recv)
+    int nranks = 0;
+    fix128 *d_gathered = nullptr;
+    bool own_gathered = false;
+    void *d_halo[4] = {nullptr, nullptr, nullptr, nullptr};
+    struct RcclComm *comm = nullptr;
+    bool in_group = false;
 };
 
 namespace {
@@ -605,6 +680,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.step0 = o.step0; P.step_decay = o.step_decay;
     P.guard = o.guard_a;
     P.MNL = c->MNL;
+    P.n_off = c->n_off; P.own_lo = c->own_lo; P.own_hi = c->own_hi; P.Ng = c->Ng;
     return P;
 }
 
@@ -617,7 +693,9 @@ FinParams fin_params(const gqmap_ctx *c)
     F.L = c->L;
     F.ctl = c->d_ctl;
     F.trace = c->d_trace;
-    F.count = (double)(c->M - 2) * (double)(c->N - 2) * c->L;
+    F.count = (double)(c->M - 2) * (double)(c->Ng - 2) * c->L;  // global interior
+    F.gathered = c->d_gathered;
+    F.nranks = c->nranks;
     F.step0 = o.step0; F.step_decay = o.step_decay;
     F.alpha_mode = o.alpha_mode; F.alpha_start = o.alpha_start; F.alpha_lr = o.alpha_lr;
     F.t_decay_every = o.t_decay_every; F.drate = o.drate; F.t_min = o.t_min; F.tor = o.tor;
@@ -654,6 +732,128 @@ void launch_iter(gqmap_ctx *c)
 
 void launch_finalize(gqmap_ctx *c) { k_finalize<<<1, 256, 0, c->stream>>>(fin_params(c)); }
 
+// ---- RCCL, resolved at first use from librccl.so.1 (the copy torch has
+// already loaded, when it has) so the library itself carries no link-time
+// dependency on it.
+struct Rccl {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char *(*GetErrorString)(ncclResult_t) = nullptr;
+    bool ok = false;
+};
+
+const Rccl *rccl()
+{
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return;
+        auto sym = [&](auto &fn, const char *name) { fn = reinterpret_cast<std::decay_t<decltype(fn)>>(dlsym(h, name)); };
+        sym(r.GetUniqueId, "ncclGetUniqueId");
+        sym(r.CommInitRank, "ncclCommInitRank");
+        sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.GroupStart, "ncclGroupStart");
+        sym(r.GroupEnd, "ncclGroupEnd");
+        sym(r.Send, "ncclSend");
+        sym(r.Recv, "ncclRecv");
+        sym(r.AllGather, "ncclAllGather");
+        sym(r.GetErrorString, "ncclGetErrorString");
+        r.ok = r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.GroupStart && r.GroupEnd && r.Send &&
+               r.Recv && r.AllGather && r.GetErrorString;
+    });
+    return &r;
+}
+
+#define GQ_NCCL(call)                                                                       \
+    do {                                                                                    \
+        ncclResult_t r_ = (call);                                                           \
+        if (r_ != ncclSuccess) {                                                            \
+            gq::set_error("%s:%d %s failed: %s", __FILE__, __LINE__, #call,                \
+                          rccl()->GetErrorString(r_));                                      \
+            return GQMAP_ERR_HIP;                                                           \
+        }                                                                                   \
+    } while (0)
+
+}  // namespace
+
+struct RcclComm {
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0;
+};
+
+namespace {
+
+template <typename R>
+void halo_copy(gqmap_ctx *c, int col, void *buf, bool to_buf)
+{
+    const int64_t n = (int64_t)NPLANES * c->L * c->M;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
+    k_halo_copy<R><<<grid, 256, 0, c->stream>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M,
+                                                (int64_t)c->M * c->N, c->MNL, c->L, col, (R *)buf, to_buf);
+}
+
+void halo_pack(gqmap_ctx *c, int col, void *buf)
+{
+    if (c->fp32) halo_copy<float>(c, col, buf, true);
+    else halo_copy<double>(c, col, buf, true);
+}
+
+void halo_unpack(gqmap_ctx *c, int col, void *buf)
+{
+    if (c->fp32) halo_copy<float>(c, col, buf, false);
+    else halo_copy<double>(c, col, buf, false);
+}
+
+// One iteration on the context's stream.  Whole grid: k_iter + k_finalize.
+// RCCL tile: k_iter, own totals, pack the boundary columns, one RCCL group
+// (in-place all-gather of the totals + ghost-column send/recv with the
+// neighbour ranks), unpack, k_finalize over all tiles' totals.
+gqmap_status launch_tail(gqmap_ctx *c)
+{
+    if (c->comm) {
+        const int NP = NFIX + c->L, r = c->comm->rank, n = c->comm->nranks;
+        k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)r * NP,
+                                                 c->d_ctl);
+        const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
+        if (left) halo_pack(c, c->own_lo, c->d_halo[0]);
+        if (right) halo_pack(c, c->own_hi - 1, c->d_halo[1]);
+        const size_t cnt = (size_t)NPLANES * c->L * c->M;
+        const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
+        const Rccl *R = rccl();
+        GQ_NCCL(R->GroupStart());
+        GQ_NCCL(R->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
+                             c->comm->comm, c->stream));
+        if (left) {
+            GQ_NCCL(R->Send(c->d_halo[0], cnt, dt, r - 1, c->comm->comm, c->stream));
+            GQ_NCCL(R->Recv(c->d_halo[2], cnt, dt, r - 1, c->comm->comm, c->stream));
+        }
+        if (right) {
+            GQ_NCCL(R->Send(c->d_halo[1], cnt, dt, r + 1, c->comm->comm, c->stream));
+            GQ_NCCL(R->Recv(c->d_halo[3], cnt, dt, r + 1, c->comm->comm, c->stream));
+        }
+        GQ_NCCL(R->GroupEnd());
+        (void)n;
+        if (left) halo_unpack(c, 0, c->d_halo[2]);
+        if (right) halo_unpack(c, c->N - 1, c->d_halo[3]);
+    }
+    launch_finalize(c);
+    return GQMAP_OK;
+}
+
+gqmap_status launch_step(gqmap_ctx *c)
+{
+    launch_iter(c);
+    return launch_tail(c);
+}
+
 gqmap_status upload_ctl(gqmap_ctx *c, int it, double T, const double *w, const double *alpha)
 {
     Ctl h{};
@@ -682,11 +882,14 @@ gqmap_status ensure_graph(gqmap_ctx *c)
     if (c->graph) return GQMAP_OK;
     hipGraph_t g;
     GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < GRAPH_CHUNK; ++i) {
-        launch_iter(c);
-        launch_finalize(c);
+    gqmap_status st = GQMAP_OK;
+    for (int i = 0; i < GRAPH_CHUNK && st == GQMAP_OK; ++i) st = launch_step(c);
+    hipError_t ec = hipStreamEndCapture(c->stream, &g);
+    if (st != GQMAP_OK) {
+        if (ec == hipSuccess) (void)hipGraphDestroy(g);
+        return st;
     }
-    GQ_HIP(hipStreamEndCapture(c->stream, &g));
+    GQ_HIP(ec);
     hipError_t e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     GQ_HIP(e);
@@ -743,14 +946,27 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
     if (c->super_)
         GQ_CHECK(Mo % 4 == 0 && No % 4 == 0, GQMAP_ERR_INVALID_ARG,
                  "super engine needs Mo,No divisible by 4 (got %dx%d)", Mo, No);
-    const int M = c->super_ ? Mo / 4 : Mo, N = c->super_ ? No / 4 : No;
-    GQ_CHECK(M >= 3 && N >= 3, GQMAP_ERR_INVALID_ARG, "node grid %dx%d has no interior", M, N);
+    const int M = c->super_ ? Mo / 4 : Mo, Ng = c->super_ ? No / 4 : No;
+    GQ_CHECK(M >= 3 && Ng >= 3, GQMAP_ERR_INVALID_ARG, "node grid %dx%d has no interior", M, Ng);
+    GQ_CHECK(Ng >= c->n_tiles, GQMAP_ERR_INVALID_ARG, "%d node columns cannot feed %d tiles", Ng,
+             c->n_tiles);
+    // column strip [col0, col1) + one ghost column per neighbour
+    const int col0 = (int)((int64_t)Ng * c->tile / c->n_tiles);
+    const int col1 = (int)((int64_t)Ng * (c->tile + 1) / c->n_tiles);
+    const int gl = c->tile > 0, gr = c->tile < c->n_tiles - 1;
+    const int N = (col1 - col0) + gl + gr;
     DeviceGuard dg(c->device);
     const bool resize = Mo != c->Mo || No != c->No || vv32 != c->vv32 || !c->d_VV;
     c->Mo = Mo;
     c->No = No;
     c->M = M;
     c->N = N;
+    c->Ng = Ng;
+    c->col0 = col0;
+    c->col1 = col1;
+    c->n_off = col0 - gl;
+    c->own_lo = gl;
+    c->own_hi = gl + (col1 - col0);
     c->MNL = (int64_t)c->M * c->N * c->L;
     c->vv32 = vv32;
     if (resize) {
@@ -763,6 +979,14 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
         gqmap_status s = alloc_grid(c);
         if (s != GQMAP_OK) return s;
         c->have_state = false;
+        if (c->n_tiles > 1) {
+            const size_t hb = (size_t)NPLANES * c->L * c->M * c->rsz;
+            for (int k = 0; k < 4; ++k) {
+                if (c->d_halo[k]) (void)hipFree(c->d_halo[k]);
+                c->d_halo[k] = nullptr;
+                GQ_HIP(hipMalloc(&c->d_halo[k], hb));
+            }
+        }
     }
     return GQMAP_OK;
 }
@@ -981,10 +1205,12 @@ gqmap_status gqmap_init_state(gqmap_ctx *c, uint64_t seed)
     const uint64_t b3 = stream_base(seed, 3), b4 = stream_base(seed, 4);
     if (c->fp32)
         k_init_state<float><<<blocks, threads, 0, c->stream>>>(
-            (float *)c->d_st[0], (float *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv, o.sig_init);
+            (float *)c->d_st[0], (float *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv, o.sig_init,
+            c->M, c->N, c->n_off, c->Ng);
     else
         k_init_state<double><<<blocks, threads, 0, c->stream>>>(
-            (double *)c->d_st[0], (double *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv, o.sig_init);
+            (double *)c->d_st[0], (double *)c->d_st[1], c->MNL, b1, b2, b3, b4, o.minu, o.maxu, o.minv, o.maxv, o.sig_init,
+            c->M, c->N, c->n_off, c->Ng);
     GQ_HIP(hipGetLastError());
     double w[GQMAP_LMAX], alpha[GQMAP_LMAX], se = 0;
     gqmap_rand_uniform(seed, 0, 0, (size_t)c->L, w);  // w = rand(1,1,L)
@@ -1005,15 +1231,23 @@ gqmap_status gqmap_set_state(gqmap_ctx *c, const gqmap_state *st)
              GQMAP_ERR_INVALID_ARG, "gqmap_set_state: null state array");
     GQ_CHECK(st->it >= 1, GQMAP_ERR_INVALID_ARG, "state.it must be >= 1");
     DeviceGuard dg(c->device);
+    // state arrays are the FULL node grid (M x Ng x L); a tile takes its
+    // columns n_off .. n_off+N-1 (owned + ghosts): one run of M*N per (plane, l)
+    const int64_t MNg = (int64_t)c->M * c->Ng, MNgL = MNg * c->L, MN = (int64_t)c->M * c->N;
     const double *planes[NPLANES] = {st->muu, st->muv, st->sigu, st->sigv, st->pn,
-                                     st->rou, st->rou + c->MNL, st->rou + 2 * c->MNL,
-                                     st->rou + 3 * c->MNL};
-    for (int b = 0; b < 2; ++b)
-        for (int q = 0; q < NPLANES; ++q) {
-            gqmap_status s = upload(c, (char *)c->d_st[b] + (size_t)q * c->MNL * c->rsz, planes[q],
+                                     st->rou, st->rou + MNgL, st->rou + 2 * MNgL,
+                                     st->rou + 3 * MNgL};
+    std::vector<double> loc((size_t)c->MNL);
+    for (int q = 0; q < NPLANES; ++q) {
+        for (int l = 0; l < c->L; ++l)
+            std::memcpy(&loc[(size_t)(l * MN)], planes[q] + l * MNg + (int64_t)c->n_off * c->M,
+                        sizeof(double) * (size_t)MN);
+        for (int b = 0; b < 2; ++b) {
+            gqmap_status s = upload(c, (char *)c->d_st[b] + (size_t)q * c->MNL * c->rsz, loc.data(),
                                     (size_t)c->MNL);
             if (s != GQMAP_OK) return s;
         }
+    }
     gqmap_status s = upload_ctl(c, st->it, st->T, st->w, st->alpha);
     if (s != GQMAP_OK) return s;
     c->have_state = true;
@@ -1030,14 +1264,21 @@ gqmap_status gqmap_get_state(gqmap_ctx *c, gqmap_state *st)
     gqmap_status s = read_ctl(c, &h);
     if (s != GQMAP_OK) return s;
     const void *cur = c->d_st[h.done & 1];
+    // full-grid arrays: a tile writes its owned columns only
+    const int64_t MNg = (int64_t)c->M * c->Ng, MNgL = MNg * c->L, MN = (int64_t)c->M * c->N;
     double *planes[NPLANES] = {st->muu, st->muv, st->sigu, st->sigv, st->pn, st->rou,
-                               st->rou ? st->rou + c->MNL : nullptr,
-                               st->rou ? st->rou + 2 * c->MNL : nullptr,
-                               st->rou ? st->rou + 3 * c->MNL : nullptr};
+                               st->rou ? st->rou + MNgL : nullptr,
+                               st->rou ? st->rou + 2 * MNgL : nullptr,
+                               st->rou ? st->rou + 3 * MNgL : nullptr};
+    std::vector<double> loc((size_t)c->MNL);
+    const size_t own = (size_t)c->M * (c->own_hi - c->own_lo);
     for (int q = 0; q < NPLANES; ++q) {
         if (!planes[q]) continue;
-        s = download(c, planes[q], (const char *)cur + (size_t)q * c->MNL * c->rsz, (size_t)c->MNL);
+        s = download(c, loc.data(), (const char *)cur + (size_t)q * c->MNL * c->rsz, (size_t)c->MNL);
         if (s != GQMAP_OK) return s;
+        for (int l = 0; l < c->L; ++l)
+            std::memcpy(planes[q] + l * MNg + (int64_t)c->col0 * c->M,
+                        &loc[(size_t)(l * MN + (int64_t)c->own_lo * c->M)], sizeof(double) * own);
     }
     for (int l = 0; l < c->L; ++l) {
         if (st->w) st->w[l] = h.w[l];
@@ -1067,6 +1308,9 @@ gqmap_status gqmap_run(gqmap_ctx *c, int n_iter, int *n_done, double *trace)
     clear_error();
     GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
     GQ_CHECK(c->have_images && c->have_state, GQMAP_ERR_STATE, "gqmap_run before images/state");
+    GQ_CHECK(c->n_tiles == 1 || c->comm, GQMAP_ERR_STATE,
+             "tile %d/%d: attach RCCL (gqmap_tile_attach_rccl) or use gqmap_tile_group_run", c->tile,
+             c->n_tiles);
     GQ_CHECK(n_iter >= 0, GQMAP_ERR_INVALID_ARG, "n_iter < 0");
     DeviceGuard dg(c->device);
     Ctl h0;
@@ -1085,10 +1329,8 @@ gqmap_status gqmap_run(gqmap_ctx *c, int n_iter, int *n_done, double *trace)
                 left -= GRAPH_CHUNK;
             }
         }
-        for (; left > 0; --left) {
-            launch_iter(c);
-            launch_finalize(c);
-        }
+        for (; left > 0; --left)
+            if ((s = launch_step(c)) != GQMAP_OK) return s;
         GQ_HIP(hipGetLastError());
         Ctl h;
         if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
@@ -1108,6 +1350,9 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     clear_error();
     GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
     GQ_CHECK(c->have_images && c->have_state, GQMAP_ERR_STATE, "gqmap_run before images/state");
+    GQ_CHECK(c->n_tiles == 1 || c->comm, GQMAP_ERR_STATE,
+             "tile %d/%d: attach RCCL (gqmap_tile_attach_rccl) or use gqmap_tile_group_run", c->tile,
+             c->n_tiles);
     GQ_CHECK(n_iter >= 1, GQMAP_ERR_INVALID_ARG, "n_iter < 1");
     DeviceGuard dg(c->device);
     Ctl h0;
@@ -1120,7 +1365,7 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
         GQ_HIP(hipEventRecord(ev[2 + 2 * i], c->stream));
         launch_iter(c);
         GQ_HIP(hipEventRecord(ev[3 + 2 * i], c->stream));
-        launch_finalize(c);
+        if ((s = launch_tail(c)) != GQMAP_OK) return s;
     }
     GQ_HIP(hipEventRecord(ev[1], c->stream));
     GQ_HIP(hipEventSynchronize(ev[1]));
@@ -1148,8 +1393,9 @@ gqmap_status gqmap_get_info(gqmap_ctx *c, gqmap_info *info)
     GQ_CHECK(c && info, GQMAP_ERR_INVALID_ARG, "null argument");
     DeviceGuard dg(c->device);
     std::memset(info, 0, sizeof(*info));
-    info->Mo = c->Mo; info->No = c->No; info->M = c->M; info->N = c->N;
+    info->Mo = c->Mo; info->No = c->No; info->M = c->M; info->N = c->have_images ? c->Ng : 0;
     info->L = c->L; info->K = c->K; info->device = c->device; info->split = c->split;
+    info->n_tiles = c->n_tiles; info->tile = c->tile; info->col0 = c->col0; info->col1 = c->col1;
     if (c->have_state) {
         Ctl h;
         gqmap_status s = read_ctl(c, &h);
@@ -1172,18 +1418,26 @@ gqmap_status gqmap_get_map(gqmap_ctx *c, double *map)
     if (s != GQMAP_OK) return s;
     const void *cur = c->d_st[h.done & 1];
     const size_t MN = (size_t)c->M * c->N;
+    std::vector<double> loc(2 * MN);
     if (c->L == 1) {  // map = cat(3, mu_u, mu_v)  (gqmap_gpu_mixture.m:55)
-        if ((s = download(c, map, cur, MN)) != GQMAP_OK) return s;
-        return download(c, map + MN, (const char *)cur + (size_t)c->MNL * c->rsz, MN);
+        if ((s = download(c, loc.data(), cur, MN)) != GQMAP_OK) return s;
+        if ((s = download(c, loc.data() + MN, (const char *)cur + (size_t)c->MNL * c->rsz, MN)) != GQMAP_OK)
+            return s;
+    } else {
+        double *d_out = nullptr;
+        GQ_HIP(hipMalloc(&d_out, sizeof(double) * 2 * MN));
+        hipError_t e = mixture_map_device(h.alpha, cur, c->fp32, c->MNL, c->M, c->N, c->L, d_out, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(loc.data(), d_out, sizeof(double) * 2 * MN, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        (void)hipFree(d_out);
+        GQ_HIP(e);
     }
-    double *d_out = nullptr;
-    GQ_HIP(hipMalloc(&d_out, sizeof(double) * 2 * MN));
-    hipError_t e = mixture_map_device(h.alpha, cur, c->fp32, c->MNL, c->M, c->N, c->L, d_out, c->stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(map, d_out, sizeof(double) * 2 * MN, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(d_out);
-    GQ_HIP(e);
+    // full-grid M x Ng x 2 output: a tile writes its owned columns
+    const size_t MNg = (size_t)c->M * c->Ng, own = (size_t)c->M * (c->own_hi - c->own_lo);
+    for (int k = 0; k < 2; ++k)
+        std::memcpy(map + k * MNg + (size_t)c->col0 * c->M, loc.data() + k * MN + (size_t)c->own_lo * c->M,
+                    sizeof(double) * own);
     return GQMAP_OK;
 }
 
@@ -1192,6 +1446,7 @@ gqmap_status gqmap_log_p(gqmap_ctx *c, const double *map, double *logp)
     clear_error();
     GQ_CHECK(c && map && logp, GQMAP_ERR_INVALID_ARG, "null argument");
     GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "no images");
+    GQ_CHECK(c->n_tiles == 1, GQMAP_ERR_UNSUPPORTED, "gqmap_log_p on a tile: evaluate on the whole grid");
     DeviceGuard dg(c->device);
     const size_t MN = (size_t)c->M * c->N;
     const int blocks = (int)((MN + 255) / 256);
@@ -1254,12 +1509,149 @@ gqmap_status gqmap_synchronize(gqmap_ctx *c)
     return GQMAP_OK;
 }
 
+gqmap_status gqmap_create_tile(gqmap_ctx **out, const gqmap_options *opt, int device, int n_tiles, int tile)
+{
+    clear_error();
+    GQ_CHECK(n_tiles >= 1 && n_tiles <= 1024, GQMAP_ERR_INVALID_ARG, "n_tiles=%d outside [1,1024]", n_tiles);
+    GQ_CHECK(tile >= 0 && tile < n_tiles, GQMAP_ERR_INVALID_ARG, "tile %d of %d", tile, n_tiles);
+    gqmap_status s = gqmap_create(out, opt, device);
+    if (s != GQMAP_OK) return s;
+    (*out)->n_tiles = n_tiles;
+    (*out)->tile = tile;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_comm_unique_id(uint8_t id[128])
+{
+    clear_error();
+    GQ_CHECK(id, GQMAP_ERR_INVALID_ARG, "null id");
+    const Rccl *R = rccl();
+    GQ_CHECK(R->ok, GQMAP_ERR_UNSUPPORTED, "librccl.so.1 not loadable: %s", dlerror());
+    ncclUniqueId u;
+    GQ_NCCL(R->GetUniqueId(&u));
+    static_assert(sizeof(u) == 128, "ncclUniqueId size");
+    std::memcpy(id, &u, 128);
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
+{
+    clear_error();
+    GQ_CHECK(c && id, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "attach after gqmap_set_images");
+    GQ_CHECK(!c->comm && !c->in_group, GQMAP_ERR_STATE, "tile already has a transport");
+    const Rccl *R = rccl();
+    GQ_CHECK(R->ok, GQMAP_ERR_UNSUPPORTED, "librccl.so.1 not loadable");
+    DeviceGuard dg(c->device);
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    RcclComm *cm = new RcclComm();
+    cm->nranks = c->n_tiles;
+    cm->rank = c->tile;
+    const ncclResult_t r = R->CommInitRank(&cm->comm, cm->nranks, u, cm->rank);
+    if (r != ncclSuccess) {
+        delete cm;
+        set_error("ncclCommInitRank(%d ranks, rank %d): %s", c->n_tiles, c->tile, R->GetErrorString(r));
+        return GQMAP_ERR_HIP;
+    }
+    const size_t NP = NFIX + c->L;
+    GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles));
+    GQ_HIP(hipMemset(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles));
+    c->own_gathered = true;
+    c->nranks = c->n_tiles;
+    c->comm = cm;
+    drop_graph(c);
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n, int n_iter, int *n_done, double *trace)
+{
+    clear_error();
+    GQ_CHECK(tiles && n >= 1 && n_iter >= 0, GQMAP_ERR_INVALID_ARG, "gqmap_tile_group_run: bad arguments");
+    gqmap_ctx *t0 = tiles[0];
+    for (int t = 0; t < n; ++t) {
+        gqmap_ctx *c = tiles[t];
+        GQ_CHECK(c && c->n_tiles == n && c->tile == t, GQMAP_ERR_INVALID_ARG,
+                 "tiles[%d] is not tile %d of %d", t, t, n);
+        GQ_CHECK(c->device == t0->device && c->fp32 == t0->fp32 && c->L == t0->L && c->M == t0->M &&
+                     c->Ng == t0->Ng,
+                 GQMAP_ERR_INVALID_ARG, "tiles of one group must share device, precision and grid");
+        GQ_CHECK(c->have_images && c->have_state && !c->comm, GQMAP_ERR_STATE,
+                 "tile %d: images/state missing or RCCL attached", t);
+    }
+    DeviceGuard dg(t0->device);
+    const int NP = NFIX + t0->L;
+    if (!t0->in_group) {  // shared totals table owned by tile 0
+        GQ_HIP(hipMalloc((void **)&t0->d_gathered, sizeof(fix128) * NP * n));
+        t0->own_gathered = true;
+        for (int t = 0; t < n; ++t) {
+            tiles[t]->d_gathered = t0->d_gathered;
+            tiles[t]->nranks = n;
+            tiles[t]->in_group = true;
+        }
+    }
+    // every launch of the group goes to tile 0's stream (restored below)
+    std::vector<hipStream_t> saved(n);
+    for (int t = 0; t < n; ++t) {
+        saved[t] = tiles[t]->stream;
+        tiles[t]->stream = t0->stream;
+    }
+    Ctl h0;
+    gqmap_status s = read_ctl(t0, &h0);
+    const size_t hb = (size_t)NPLANES * t0->L * t0->M * t0->rsz;
+    for (int i = 0; i < n_iter && s == GQMAP_OK; ++i) {
+        for (int t = 0; t < n; ++t) launch_iter(tiles[t]);
+        for (int t = 0; t < n; ++t) {
+            gqmap_ctx *c = tiles[t];
+            k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)t * NP,
+                                                     c->d_ctl);
+            if (t > 0) halo_pack(c, c->own_lo, c->d_halo[0]);
+            if (t < n - 1) halo_pack(c, c->own_hi - 1, c->d_halo[1]);
+        }
+        for (int t = 0; t < n && s == GQMAP_OK; ++t) {
+            if (t < n - 1 && hipMemcpyAsync(tiles[t + 1]->d_halo[2], tiles[t]->d_halo[1], hb, hipMemcpyDeviceToDevice,
+                                            t0->stream) != hipSuccess)
+                s = GQMAP_ERR_HIP;
+            if (t > 0 && hipMemcpyAsync(tiles[t - 1]->d_halo[3], tiles[t]->d_halo[0], hb, hipMemcpyDeviceToDevice,
+                                        t0->stream) != hipSuccess)
+                s = GQMAP_ERR_HIP;
+        }
+        for (int t = 0; t < n; ++t) {
+            gqmap_ctx *c = tiles[t];
+            if (t > 0) halo_unpack(c, 0, c->d_halo[2]);
+            if (t < n - 1) halo_unpack(c, c->N - 1, c->d_halo[3]);
+        }
+        for (int t = 0; t < n; ++t) launch_finalize(tiles[t]);
+        if (hipGetLastError() != hipSuccess) s = GQMAP_ERR_HIP;
+        if (i % 64 == 63 && s == GQMAP_OK) {  // stop test (and bounded queue depth)
+            Ctl h;
+            if ((s = read_ctl(t0, &h)) == GQMAP_OK && h.stop) break;
+        }
+    }
+    if (s != GQMAP_OK && !gqmap_last_error()[0]) set_error("gqmap_tile_group_run: HIP launch failed");
+    Ctl h;
+    if (s == GQMAP_OK) s = read_ctl(t0, &h);
+    for (int t = 0; t < n; ++t) tiles[t]->stream = saved[t];
+    if (s != GQMAP_OK) return s;
+    const int ran = h.it - h0.it;
+    if ((s = fetch_trace(t0, h0.it, std::min(ran, TRACE_CAP), trace)) != GQMAP_OK) return s;
+    if (n_done) *n_done = ran;
+    return GQMAP_OK;
+}
+
 void gqmap_destroy(gqmap_ctx *c)
 {
     if (!c) return;
     DeviceGuard dg(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graph(c);
+    if (c->comm) {
+        (void)rccl()->CommDestroy(c->comm->comm);
+        delete c->comm;
+    }
+    if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);
+    for (void *p : c->d_halo)
+        if (p) (void)hipFree(p);
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace};
     for (void *p : bufs)
         if (p) (void)hipFree(p);

@@ -116,12 +116,16 @@ class Engine:
     """One device context (gqmap_ctx) holding images and state on the GPU."""
 
     def __init__(self, options: dict, I1, I2, engine: str = "mixture", precision: str = "fp64",
-                 device: int = 0):
+                 device: int = 0, n_tiles: int = 1, tile: int = 0):
         self.lib = _lib.load()
         self.engine, self.precision = engine, precision
         self.opts = make_options(options, engine, precision)
         self.ctx = C.c_void_p()
-        check(self.lib.gqmap_create(C.byref(self.ctx), C.byref(self.opts), device), "gqmap_create")
+        if n_tiles == 1:
+            check(self.lib.gqmap_create(C.byref(self.ctx), C.byref(self.opts), device), "gqmap_create")
+        else:
+            check(self.lib.gqmap_create_tile(C.byref(self.ctx), C.byref(self.opts), device, n_tiles, tile),
+                  "gqmap_create_tile")
         I1, I2 = f64(I1), f64(I2)
         if I1.shape != I2.shape or I1.ndim != 2:
             raise ValueError("I1 and I2 must be equal-size 2-D images")
@@ -129,7 +133,14 @@ class Engine:
         check(self.lib.gqmap_set_images(self.ctx, dptr(I1), dptr(I2), self.Mo, self.No),
               "gqmap_set_images")
         info = self.info()
-        self.M, self.N, self.L = info.M, info.N, info.L
+        self.M, self.N, self.L = info.M, info.N, info.L  # full node grid (a tile owns col0:col1)
+        self.n_tiles, self.tile, self.col0, self.col1 = info.n_tiles, info.tile, info.col0, info.col1
+
+    # -- multi-GPU tiles ---------------------------------------------------
+    def attach_rccl(self, unique_id: bytes) -> None:
+        """Join the RCCL communicator of all tiles (rank == tile); collective."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
+        check(self.lib.gqmap_tile_attach_rccl(self.ctx, buf), "gqmap_tile_attach_rccl")
 
     # -- state -----------------------------------------------------------
     def init_state(self, seed: int = 0) -> None:
@@ -199,6 +210,25 @@ class Engine:
 
     def __exit__(self, *a):
         self.close()
+
+
+def comm_unique_id() -> bytes:
+    """An RCCL unique id for Engine.attach_rccl (draw on one rank, broadcast)."""
+    buf = (C.c_uint8 * 128)()
+    check(_lib.load().gqmap_comm_unique_id(buf), "gqmap_comm_unique_id")
+    return bytes(buf)
+
+
+def tile_group_run(tiles, n_iter: int):
+    """Run the tiles of one grid (same device, tile order) n_iter iterations in
+    lockstep with in-process halo exchange.  Returns (n_done, trace)."""
+    lib = _lib.load()
+    arr = (C.c_void_p * len(tiles))(*[t.ctx.value for t in tiles])
+    trace = np.zeros((max(n_iter, 1), 3))
+    done = C.c_int(0)
+    check(lib.gqmap_tile_group_run(arr, len(tiles), int(n_iter), C.byref(done), dptr(trace)),
+          "gqmap_tile_group_run")
+    return done.value, trace[:done.value]
 
 
 def aepe(tflow: np.ndarray, flow: np.ndarray, unknown: np.ndarray, crop: int = 1) -> float:

@@ -107,6 +107,8 @@ typedef struct gqmap_info {
     double T;
     int device;
     int split;           /* lanes per node Q in use                             */
+    int n_tiles, tile;   /* column-strip tiling (1, 0 for a whole-grid context) */
+    int col0, col1;      /* node columns [col0, col1) owned by this context     */
 } gqmap_info;
 
 typedef struct gqmap_ctx gqmap_ctx;
@@ -140,6 +142,32 @@ gqmap_status gqmap_get_map(gqmap_ctx *ctx, double *map);
 gqmap_status gqmap_log_p(gqmap_ctx *ctx, const double *map, double *logp);
 gqmap_status gqmap_synchronize(gqmap_ctx *ctx);
 void gqmap_destroy(gqmap_ctx *ctx);
+
+/* ---- multi-GPU: column-strip tiles with ghost-column (halo) exchange ----
+ * The node grid is split into n_tiles strips of whole columns (contiguous in
+ * the column-major layout); tile t owns node columns
+ * [floor(Ng*t/n), floor(Ng*(t+1)/n)) and keeps one ghost column per
+ * neighbour.  Every iteration the tiles exchange their boundary columns (all
+ * 9 state planes) and the per-tile exact fixed-point totals (Energy, sums of
+ * |dmu|, |dsigma|, dalpha), so a tiled solve is bit-identical to the whole-
+ * grid solve (§8(e) of SURVEY.md: gqmap_gpu_mixture.m:29-46 is Jacobi).
+ * A tile context takes the FULL frames in gqmap_set_images (replicated: the
+ * bicubic samples reach far outside the strip), and FULL-grid state arrays
+ * in gqmap_set_state / gqmap_get_state / gqmap_get_map (set reads the tile's
+ * columns, get writes the owned columns only).  gqmap_log_p is whole-grid. */
+gqmap_status gqmap_create_tile(gqmap_ctx **ctx, const gqmap_options *opt, int device, int n_tiles,
+                               int tile);
+/* RCCL transport (one process per GPU): rank 0 draws the id, the caller
+ * broadcasts it (e.g. torch.distributed), every tile attaches with rank ==
+ * tile.  Collective: blocks until all n_tiles ranks have attached.  After it,
+ * gqmap_run / gqmap_run_timed exchange over RCCL on the context's stream. */
+gqmap_status gqmap_comm_unique_id(uint8_t id[128]);
+gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *ctx, const uint8_t id[128]);
+/* In-process transport: tiles[0..n_tiles-1] (tile index order, one device)
+ * run n_iter iterations in lockstep, exchanging through device copies.
+ * trace as gqmap_run (tile 0's copy; every tile computes the same). */
+gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n_tiles, int n_iter, int *n_done,
+                                  double *trace);
 
 /* ---- standalone device ops (host pointers in/out) ---- */
 /* projsplx.m:15-30, applied independently to each of `ncols` columns of Y

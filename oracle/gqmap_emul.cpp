@@ -53,7 +53,16 @@ struct Work {
     std::vector<Grad<R>> node, edge;         // node [MNL], edge [MNL*4] (e = dir + 2*uv)
 };
 
-inline bool interior(int m, int n, int M, int N) { return m >= 1 && m <= M - 2 && n >= 1 && n <= N - 2; }
+// Column-strip tile geometry (gqmap_create_tile): local column n is global
+// column n + n_off of Ng; only [own_lo, own_hi) is updated.  Whole grid:
+// n_off = 0, [0, N), Ng = N.
+struct Geo {
+    int n_off, own_lo, own_hi, Ng;
+    bool upd(int m, int n, int M) const
+    {
+        return m >= 1 && m <= M - 2 && n >= own_lo && n < own_hi && n + n_off >= 1 && n + n_off <= Ng - 2;
+    }
+};
 inline bool finite_d(double x) { return std::isfinite(x); }
 
 // one term's quadrature sum split over Q lanes (k = j, j+Q, ...) + butterfly
@@ -69,7 +78,7 @@ auto split_sums(int Q, F part) -> decltype(part(0, 1))
 template <typename R, int ENG>
 int run_t(const orc_params *P, const double *X, const double *W, const double *I1,
           const double *VV, orc_state *S, double *T_io, int it_first, int n_iter, double *trace,
-          int Q)
+          int Q, const Geo &G, int64_t *totals_out)
 {
     Work<R> w;
     w.P = P;
@@ -128,12 +137,12 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                 const R a = R(S->alpha[l]);
                 for (int m = 0; m < M; ++m) {
                     const int64_t i = m + (int64_t)M * n + MN * l;
-                    const bool inner = interior(m, n, M, N);
+                    const bool inner = G.upd(m, n, M);
                     if (inner) {
                         const NodeCoef<R> c = node_coef(st[i + 2 * MNL], st[i + 3 * MNL], st[i + 4 * MNL]);
                         const Sums<R> Sn = split_sums(Q, [&](int k0, int dk) {
                             return node_sums<ENG>(tab, k0, w.K2, dk, VVp, I1p, w.M2, w.Mo, w.No, eps,
-                                                  c, st[i], st[i + MNL], m, n);
+                                                  c, st[i], st[i + MNL], m, n + G.n_off);
                         });
                         w.node[i] = node_epi(Sn, c, lamd, guard, Tr, a, st[i + 2 * MNL],
                                              st[i + 3 * MNL], st[i + 4 * MNL], ENG == 2);
@@ -141,7 +150,7 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                     for (int e = 0; e < 4; ++e) {
                         const int dir = e & 1, uv = e >> 1;
                         const int rm = dir == 0 ? m + 1 : m, rn = dir == 1 ? n + 1 : n;
-                        const bool r_inner = rm < M && rn < N && interior(rm, rn, M, N);
+                        const bool r_inner = rm < M && rn < N && G.upd(rm, rn, M);
                         Grad<R> g{};
                         if (inner || r_inner) {
                             const int64_t r = rm + (int64_t)M * rn + MN * l;
@@ -163,9 +172,10 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
         {
             fix128 lE = 0, lmu = 0, lsg = 0, lnf = 0, lda[LMAX] = {0};
 #pragma omp for schedule(static)
-            for (int n = 1; n < N - 1; ++n)
+            for (int n = 0; n < N; ++n)
                 for (int l = 0; l < L; ++l)
                     for (int m = 1; m < M - 1; ++m) {
+                        if (!G.upd(m, n, M)) continue;
                         const int64_t i = m + (int64_t)M * n + MN * l;
                         const int64_t iu = i - 1, il = i - M;  // (m-1,n), (m,n-1)
                         const Grad<R> &nd = w.node[i];
@@ -211,11 +221,19 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
         std::swap(w.st, w.nst);
         // border nodes keep their values in both buffers
         w.nst = w.st;
+        if (totals_out) {  // this tile's exact totals, fix128 as (lo, hi) int64 pairs
+            const fix128 v[NFIX] = {fE, fmu, fsg, fnf};
+            for (int q = 0; q < NFIX + L; ++q) {
+                const fix128 x = q < NFIX ? v[q] : fda[q - NFIX];
+                totals_out[2 * q] = (int64_t)(uint64_t)x;
+                totals_out[2 * q + 1] = (int64_t)(x >> 64);
+            }
+        }
         // 3. finalize (k_finalize)
         double tot[NFIX + LMAX];
         tot[0] = from_fix(fE); tot[1] = from_fix(fmu); tot[2] = from_fix(fsg); tot[3] = from_fix(fnf);
         for (int l = 0; l < L; ++l) tot[NFIX + l] = from_fix(fda[l]);
-        const double count = (double)(M - 2) * (double)(N - 2) * L;
+        const double count = (double)(M - 2) * (double)(G.Ng - 2) * L;
         const double step_d = P->step0 / (1.0 + it / P->step_decay);
         const bool bad = tot[3] != 0.0;
         const double nan = std::nan("");
@@ -270,6 +288,35 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
 
 }  // namespace
 
+template <typename R>
+static int run_eng(const orc_params *P, const double *X, const double *W, const double *I1,
+                   const double *VV, orc_state *S, double *T_io, int it_first, int n_iter, double *trace,
+                   int Q, const Geo &G, int64_t *tot)
+{
+    if (P->ctf) return run_t<R, 2>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q, G, tot);
+    if (P->super_) return run_t<R, 1>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q, G, tot);
+    return run_t<R, 0>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q, G, tot);
+}
+
+/* One tile of a column-strip decomposition: P->N is the LOCAL node-column
+ * count (owned + ghosts), geo = {n_off, own_lo, own_hi, Ng}; the state is the
+ * local grid.  totals (2*(NFIX+L) int64) receive the last iteration's exact
+ * per-tile sums; the finalize inside uses the local sums (callers combine the
+ * tiles' totals themselves). */
+extern "C" int emu_run_tile(const orc_params *P, const double *X, const double *W, const double *I1,
+                            const double *VV, orc_state *S, double *T_io, int it_first, int n_iter,
+                            double *trace, int nthreads, int fp32, int split, const int *geo,
+                            int64_t *totals)
+{
+    if (split != 1 && split != 4 && split != 16) return -2;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    const Geo G{geo[0], geo[1], geo[2], geo[3]};
+    return fp32 ? run_eng<float>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, split, G, totals)
+                : run_eng<double>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, split, G, totals);
+}
+
 extern "C" int emu_run(const orc_params *P, const double *X, const double *W, const double *I1,
                        const double *VV, orc_state *S, double *T_io, int it_first, int n_iter,
                        double *trace, int nthreads, int fp32, int split)
@@ -279,14 +326,9 @@ extern "C" int emu_run(const orc_params *P, const double *X, const double *W, co
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
-    if (P->ctf)
-        return fp32 ? run_t<float, 2>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
-                    : run_t<double, 2>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
-    if (P->super_)
-        return fp32 ? run_t<float, 1>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
-                    : run_t<double, 1>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
-    return fp32 ? run_t<float, 0>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q)
-                : run_t<double, 0>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q);
+    const Geo G{0, 0, P->N, P->N};
+    return fp32 ? run_eng<float>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q, G, nullptr)
+                : run_eng<double>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q, G, nullptr);
 }
 
 extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)

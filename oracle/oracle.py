@@ -346,3 +346,44 @@ def ctf_pipeline(opts: dict, img1, img2, scales, init_fn, *, solver: str = "emu"
         warp = _f64(warp + flow)
         levels.append(dict(I1w=I1w, I2=I2, flow=flow, warp=warp.copy(), its=done, trace=tr))
     return warp, levels
+
+
+def tile_geometry(Ng: int, n_tiles: int, tile: int):
+    """Column strip of tile `tile` (gqmap_create_tile): (col0, col1, n_off,
+    own_lo, own_hi, N_local)."""
+    col0, col1 = Ng * tile // n_tiles, Ng * (tile + 1) // n_tiles
+    gl, gr = int(tile > 0), int(tile < n_tiles - 1)
+    return col0, col1, col0 - gl, gl, gl + (col1 - col0), (col1 - col0) + gl + gr
+
+
+def emu_run_tile(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W, geo, *,
+                 T: float | None = None, nthreads: int = 0, fp32: bool = False, split: int = 1):
+    """CPU model of one tile (local grid state incl. ghost columns, geo =
+    (n_off, own_lo, own_hi, Ng)).  Returns (done, trace, T, totals) where
+    totals are the last iteration's exact per-tile sums as Python ints
+    (value * 2^64): Energy, sum|dmu|, sum|dsigma|, #nonfinite, dalpha[L]."""
+    I1 = _f64(I1)
+    Mo, No = I1.shape
+    p = make_params(opts, Mo, No)
+    p.N = state.muu.shape[1]  # local node columns
+    VV = get_vv(I2)
+    X, W = _f64(np.asarray(X, dtype=np.float64)), _f64(np.asarray(W, dtype=np.float64))
+    Tbox = (C.c_double * 1)(p.T if T is None else T)
+    trace = np.zeros((max(n_iter, 1), 3))
+    g = (C.c_int * 4)(*[int(v) for v in geo])
+    tot = np.zeros(2 * (4 + p.L), dtype=np.int64)
+    f = lib().emu_run_tile
+    f.restype = C.c_int
+    cs = state.cstruct()
+    done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter, _p(trace),
+             nthreads, int(fp32), int(split), g, tot.ctypes.data_as(C.POINTER(C.c_int64)))
+    if done < 0:
+        raise RuntimeError("emu_run_tile failed")
+    totals = [(int(tot[2 * q]) & ((1 << 64) - 1)) + (int(tot[2 * q + 1]) << 64) for q in range(4 + p.L)]
+    return done, trace[:done].copy(), Tbox[0], totals
+
+
+def from_fix(v: int) -> float:
+    """gqmap_math.h from_fix: (double)hi + (double)lo * 2^-64 of a value * 2^64."""
+    hi, lo = v >> 64, v & ((1 << 64) - 1)
+    return float(hi) + float(lo) * 5.42101086242752217004e-20

@@ -1,0 +1,114 @@
+"""Column-strip tiles on the device (gqmap_create_tile): the in-process
+transport (gqmap_tile_group_run, several tiles on one GPU exchanging ghost
+columns and exact totals) and a one-rank RCCL communicator must reproduce
+the whole-grid engine BIT FOR BIT."""
+import numpy as np
+import pytest
+
+from tests import _golden as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(engine="mixture", L=1, M=96, N=128):
+    from gqmap_opticalflow_amd import flow_to_color, flowio
+    name = "Urban3" if engine == "super" else "rubberwhale"
+    I1, I2, gt = flowio.load_pair(name)
+    I1, I2, gt = (np.asfortranarray(a[100:100 + M, 120:120 + N]) for a in (I1, I2, gt))
+    _, _, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
+    sup = engine == "super"
+    o = dict(K=11 if sup else 9, L=L, temperature=0.2 if sup else 0.05, drate=0.75, epsn=1e-6, lambdad=1.0,
+             lambdas=16.0 if sup else 5.0, minu=minu, maxu=maxu, minv=minv, maxv=maxv, alpha_start=10,
+             t_decay_every=15)
+    return I1, I2, o
+
+
+def _whole(I1, I2, o, engine, precision, its, seed):
+    from gqmap_opticalflow_amd import Engine
+    with Engine(o, I1, I2, engine, precision) as e:
+        e.init_state(seed)
+        init = e.get_state()
+        done, tr = e.run(its)
+        return init, e.get_state(), tr
+
+
+def _assemble(tiles, getter):
+    out = None
+    for t in tiles:
+        s = getter(t)
+        if out is None:
+            out = s
+        else:
+            for k in G.STATE_KEYS[:6]:
+                getattr(out, k)[:, t.col0:t.col1] = getattr(s, k)[:, t.col0:t.col1]
+    return out
+
+
+@pytest.mark.parametrize("engine,L,precision,n_tiles", [("mixture", 1, "fp64", 2), ("mixture", 1, "fp64", 5),
+                                                        ("mixture", 3, "fp32", 3), ("super", 3, "fp64", 4),
+                                                        ("super", 2, "fp32", 2)])
+def test_tile_group_bit_exact_vs_whole_grid(engine, L, precision, n_tiles):
+    from gqmap_opticalflow_amd import Engine, tile_group_run
+    M, N = (96, 128) if engine == "mixture" else (96, 160)
+    I1, I2, o = _problem(engine, L, M, N)
+    its = 40
+    init, ref, tr = _whole(I1, I2, o, engine, precision, its, seed=3)
+    tiles = [Engine(o, I1, I2, engine, precision, n_tiles=n_tiles, tile=t) for t in range(n_tiles)]
+    try:
+        for t in tiles:
+            t.init_state(3)  # global RNG indexing: each tile draws its columns of the whole grid
+        got0 = _assemble(tiles, lambda t: t.get_state())
+        for k in G.STATE_KEYS[:6]:
+            np.testing.assert_array_equal(getattr(got0, k), getattr(init, k), err_msg="init " + k)
+        done, ttr = tile_group_run(tiles, its)
+        assert done == its
+        np.testing.assert_array_equal(ttr, tr)
+        got = _assemble(tiles, lambda t: t.get_state())
+        for k in G.STATE_KEYS:
+            np.testing.assert_array_equal(getattr(got, k), getattr(ref, k), err_msg=k)
+        mp = np.zeros((tiles[0].M, tiles[0].N, 2), order="F")
+        for t in tiles:
+            m = t.map()
+            mp[:, t.col0:t.col1] = m[:, t.col0:t.col1]
+        with Engine(o, I1, I2, engine, precision) as e:
+            e.set_state(ref)
+            np.testing.assert_array_equal(mp, e.map())
+    finally:
+        for t in tiles:
+            t.close()
+
+
+def test_tile_set_state_from_full_grid():
+    from gqmap_opticalflow_amd import Engine, tile_group_run
+    I1, I2, o = _problem()
+    init, ref, tr = _whole(I1, I2, o, "mixture", "fp64", 25, seed=5)
+    tiles = [Engine(o, I1, I2, n_tiles=3, tile=t) for t in range(3)]
+    for t in tiles:
+        t.set_state(init.copy())
+    tile_group_run(tiles, 25)
+    got = _assemble(tiles, lambda t: t.get_state())
+    for k in G.STATE_KEYS:
+        np.testing.assert_array_equal(getattr(got, k), getattr(ref, k), err_msg=k)
+    with pytest.raises(Exception, match="attach RCCL"):
+        tiles[0].run(1)
+    for t in tiles:
+        t.close()
+
+
+def test_single_rank_rccl_tile_matches_whole_grid():
+    # exercises the RCCL transport (communicator, in-place all-gather of the
+    # exact totals, graph capture of the collective) on one GPU
+    from gqmap_opticalflow_amd import Engine, comm_unique_id
+    I1, I2, o = _problem("mixture", 3)
+    init, ref, tr = _whole(I1, I2, o, "mixture", "fp64", 120, seed=1)
+    e = Engine(o, I1, I2, n_tiles=1, tile=0)
+    try:
+        e.attach_rccl(comm_unique_id())
+        e.set_state(init.copy())
+        done, t2 = e.run(120)  # two 50-iteration graph replays + 20 launches
+        np.testing.assert_array_equal(t2, tr)
+        got = e.get_state()
+        for k in G.STATE_KEYS:
+            np.testing.assert_array_equal(getattr(got, k), getattr(ref, k), err_msg=k)
+    finally:
+        e.close()

@@ -1,0 +1,181 @@
+"""Column-strip tiling (multi-GPU decomposition) on the CPU
+model of the kernel: tiles with ghost columns, exchanged every iteration, and
+per-tile exact totals summed across tiles must reproduce the whole-grid
+solve BIT FOR BIT.  The protocol is the one the RCCL transport
+(gqmap_tile_attach_rccl) and the in-process transport (gqmap_tile_group_run)
+run on the device; here it runs in one process and over torch.distributed
+gloo with two ranks."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import _golden as G
+
+
+def _case(L=1, engine="mixture", M=30, N=41):
+    from gqmap_opticalflow_amd import flowio
+    from oracle import gqmap_np
+    I1, I2, gt = flowio.load_pair("rubberwhale")
+    sup = engine == "super"
+    Mo, No = (4 * M, 4 * N) if sup else (M, N)
+    I1, I2, gt = (np.asfortranarray(a[100:100 + Mo, 150:150 + No]) for a in (I1, I2, gt))
+    _, _, (minu, maxu, minv, maxv), _ = gqmap_np.flow_to_color(gt)
+    o = dict(engine=engine, K=7, L=L, temperature=0.1, drate=0.5, epsn=1e-6, lambdad=1.0,
+             lambdas=16.0 if sup else 5.0, minu=minu, maxu=maxu, minv=minv, maxv=maxv, tor=-1.0,
+             alpha_start=1 << 30, t_decay_every=3)
+    rng = np.random.default_rng(7)
+    du, dv = maxu - minu, maxv - minv
+    f = lambda a: np.asfortranarray(a)
+    st = dict(muu=f(minu + rng.random((M, N, L)) * du), muv=f(minv + rng.random((M, N, L)) * dv),
+              sigu=f(rng.random((M, N, L)) + 1), sigv=f(rng.random((M, N, L)) + 1),
+              pn=f(0.4 * (2 * rng.random((M, N, L)) - 1)), rou=f(0.4 * (2 * rng.random((M, N, L, 2, 2)) - 1)),
+              w=np.zeros(L), alpha=np.full(L, 1.0 / L))
+    return I1, I2, o, st
+
+
+def _gh(K):
+    from oracle import oracle
+    return oracle.gauss_hermite(K)
+
+
+def _local(st, n_off, Nl):
+    from oracle import oracle
+    return oracle.State(*(np.array(st[k][:, n_off:n_off + Nl], order="F", copy=True) if k not in ("w", "alpha")
+                          else np.array(st[k], copy=True) for k in G.STATE_KEYS))
+
+
+def _whole(I1, I2, o, st, its):
+    from oracle import oracle
+    X, W = _gh(o["K"])
+    s = oracle.State(*(np.array(st[k], order="F", copy=True) for k in G.STATE_KEYS))
+    done, tr, T = oracle.emu_run(o, I1, I2, s, 1, its, X, W, split=1)
+    return s, tr
+
+
+def _tiled_one_process(I1, I2, o, st, its, n_tiles):
+    from oracle import oracle
+    X, W = _gh(o["K"])
+    M, N, L = st["muu"].shape
+    glob = {k: np.array(v, order="F", copy=True) for k, v in st.items()}
+    T = o["temperature"]
+    trace = []
+    for it in range(1, its + 1):
+        tot = [0] * (4 + L)
+        new = {k: v.copy(order="F") for k, v in glob.items()}
+        for t in range(n_tiles):
+            col0, col1, n_off, lo, hi, Nl = oracle.tile_geometry(N, n_tiles, t)
+            s = _local(glob, n_off, Nl)
+            _, _, T_next, totals = oracle.emu_run_tile(o, I1, I2, s, it, 1, X, W, (n_off, lo, hi, N), T=T)
+            tot = [a + b for a, b in zip(tot, totals)]
+            for k, a in zip(G.STATE_KEYS[:6], s.arrays()[:6]):
+                new[k][:, col0:col1] = a[:, lo:hi]
+        T = T_next
+        glob = new
+        cnt = (M - 2) * (N - 2) * L
+        trace.append((oracle.from_fix(tot[0]), oracle.from_fix(tot[1]) / cnt, oracle.from_fix(tot[2]) / cnt))
+    return glob, np.array(trace)
+
+
+@pytest.mark.parametrize("n_tiles", [2, 3, 5])
+@pytest.mark.parametrize("L,engine", [(1, "mixture"), (3, "mixture"), (2, "super")])
+def test_tiles_reproduce_whole_grid_bit_exact(oracle_lib, n_tiles, L, engine):
+    I1, I2, o, st = _case(L, engine, *((8, 11) if engine == "super" else (30, 41)))
+    its = 5
+    ref, tr = _whole(I1, I2, o, st, its)
+    glob, ttr = _tiled_one_process(I1, I2, o, st, its, n_tiles)
+    for k, a in zip(G.STATE_KEYS[:6], ref.arrays()[:6]):
+        np.testing.assert_array_equal(glob[k], a, err_msg=k)
+    np.testing.assert_array_equal(ttr, tr)
+
+
+def test_tile_geometry_matches_library_rule():
+    from oracle import oracle
+    for Ng, n in ((584, 8), (97, 3), (10, 10), (146, 4)):
+        cols = []
+        for t in range(n):
+            col0, col1, n_off, lo, hi, Nl = oracle.tile_geometry(Ng, n, t)
+            assert col1 > col0 and n_off + lo == col0 and n_off + hi == col1 and Nl == hi + (t < n - 1)
+            cols.append((col0, col1))
+        assert cols[0][0] == 0 and cols[-1][1] == Ng
+        assert all(a[1] == b[0] for a, b in zip(cols, cols[1:]))
+
+
+def _gloo_worker(rank, world, port, its, result_q):
+    import torch.distributed as dist
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        I1, I2, o, st = _case(3, "mixture")
+        X, W = _gh(o["K"])
+        M, N, L = st["muu"].shape
+        col0, col1, n_off, lo, hi, Nl = oracle.tile_geometry(N, world, rank)
+        s = _local(st, n_off, Nl)
+        T = o["temperature"]
+        trace = []
+        import torch
+        for it in range(1, its + 1):
+            _, _, T, totals = oracle.emu_run_tile(o, I1, I2, s, it, 1, X, W, (n_off, lo, hi, N), T=T)
+            # ghost columns <- the neighbours' boundary columns (all 9 planes)
+            arrs = s.arrays()[:6]
+            pack = lambda c: torch.from_numpy(np.concatenate([a[:, c].ravel(order="F") for a in arrs]))
+            def unpack(c, buf):
+                off = 0
+                for a in arrs:
+                    n = a[:, c].size
+                    a[:, c] = buf[off:off + n].numpy().reshape(a[:, c].shape, order="F")
+                    off += n
+            reqs, bufs = [], {}
+            if rank > 0:
+                bufs["l"] = torch.empty_like(pack(lo))
+                reqs += [dist.isend(pack(lo), rank - 1), dist.irecv(bufs["l"], rank - 1)]
+            if rank < world - 1:
+                bufs["r"] = torch.empty_like(pack(hi - 1))
+                reqs += [dist.isend(pack(hi - 1), rank + 1), dist.irecv(bufs["r"], rank + 1)]
+            for r in reqs:
+                r.wait()
+            if "l" in bufs:
+                unpack(0, bufs["l"])
+            if "r" in bufs:
+                unpack(Nl - 1, bufs["r"])
+            # per-tile exact totals -> every rank sums all of them
+            allt = [None] * world
+            dist.all_gather_object(allt, totals)
+            tot = [sum(x) for x in zip(*allt)]
+            cnt = (M - 2) * (N - 2) * L
+            trace.append((oracle.from_fix(tot[0]), oracle.from_fix(tot[1]) / cnt))
+        owned = [a[:, lo:hi].copy() for a in s.arrays()[:6]]
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (col0, col1, owned))
+        if rank == 0:
+            result_q.put((gathered, trace))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tiles_over_gloo_two_ranks(oracle_lib):
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    its = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, its, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered, trace = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    I1, I2, o, st = _case(3, "mixture")
+    ref, tr = _whole(I1, I2, o, st, its)
+    for k_i, (k, a) in enumerate(zip(G.STATE_KEYS[:6], ref.arrays()[:6])):
+        glob = np.zeros_like(a)
+        for col0, col1, owned in gathered:
+            glob[:, col0:col1] = owned[k_i]
+        np.testing.assert_array_equal(glob, a, err_msg=k)
+    np.testing.assert_array_equal(np.array(trace), tr[:, :2])
