@@ -1,0 +1,83 @@
+"""Summarise a profile_round.sh run into profiles/:
+  profiles/<tag>_<cfg>_<prec>_kernel_stats.csv   rocprofv3 --stats table (copied)
+  profiles/<tag>_<cfg>_<prec>_summary.txt        per-kernel avg duration, FETCH/WRITE per dispatch
+  profiles/traffic_<cfg>_<prec>.json             corrected HBM bytes per k_iter launch (bench.py)
+FETCH_SIZE is scaled by the factor measured on the calibration kernels for
+the same access width (8-B lanes for fp64 state, 4-B for fp32) against their
+known byte counts; WRITE_SIZE likewise.
+usage: python3 scripts/pmc_summary.py gpurun_out/<tag> <cfg> <prec>"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rows(path):
+    with open(path, newline="") as f:
+        yield from csv.DictReader(f)
+
+
+def find(d, name):
+    for dp, _, fs in os.walk(d):
+        for f in fs:
+            if f.endswith(name):
+                return os.path.join(dp, f)
+    return None
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    for r in rows(path):
+        if r["Counter_Name"] == counter:
+            acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    base, cfg, prec = sys.argv[1], sys.argv[2], sys.argv[3]
+    tag = os.path.basename(base.rstrip("/"))
+    d = os.path.join(base, f"{cfg}_{prec}")
+    stats = find(os.path.join(d, "trace"), "kernel_stats.csv")
+    fetch = per_kernel(find(os.path.join(d, "fetch"), "counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(find(os.path.join(d, "write"), "counter_collection.csv"), "WRITE_SIZE")
+    cal_f = per_kernel(find(os.path.join(base, "calib_fetch"), "counter_collection.csv"), "FETCH_SIZE")
+    cal_w = per_kernel(find(os.path.join(base, "calib_write"), "counter_collection.csv"), "WRITE_SIZE")
+    GiB = float(1 << 30)
+    width = "double" if prec == "fp64" else "float"
+    pick = lambda tab, kind: next((v for k, v in tab.items() if kind in k and width in k), None)
+    f_read = pick(cal_f, "k_read")    # FETCH_SIZE units are KB (rocprofv3 derived counter)
+    f_write = pick(cal_w, "k_write")
+    fcorr = GiB / (f_read * 1024) if f_read else None
+    wcorr = GiB / (f_write * 1024) if f_write else None
+    out_stats = os.path.join(ROOT, "profiles", f"{tag}_{cfg}_{prec}_kernel_stats.csv")
+    shutil.copy(stats, out_stats)
+    lines = [f"profile {tag} config {cfg} precision {prec} (bench.py --steps 200 --warmup 5 under rocprofv3)",
+             f"calibration ({width} lanes, 1 GiB): FETCH_SIZE x{fcorr:.3f}, WRITE_SIZE x{wcorr:.3f}"
+             if fcorr and wcorr else "calibration: missing", ""]
+    lines.append(f"{'kernel':70s} {'calls':>6s} {'avg_us':>10s} {'FETCH_KB':>12s} {'WRITE_KB':>12s} {'HBM_MB(corr)':>13s}")
+    traffic = None
+    for r in rows(stats):
+        name = r["Name"]
+        f = fetch.get(name)
+        w = write.get(name)
+        corr = (f * 1024 * fcorr + w * 1024 * wcorr) if (f is not None and w is not None and fcorr) else None
+        lines.append(f"{name[:70]:70s} {r['Calls']:>6s} {float(r['AverageNs']) / 1e3:10.2f} "
+                     f"{f if f is not None else float('nan'):12.1f} {w if w is not None else float('nan'):12.1f} "
+                     f"{(corr or float('nan')) / 1e6:13.3f}")
+        if "k_iter" in name and traffic is None and corr is not None:
+            traffic = dict(kernel=name, avg_us=float(r["AverageNs"]) / 1e3, fetch_kb=f, write_kb=w,
+                           fetch_corr=fcorr, write_corr=wcorr, hbm_bytes_per_launch=corr,
+                           source=f"profiles/{tag}_{cfg}_{prec}_summary.txt")
+    txt = "\n".join(lines) + "\n"
+    open(os.path.join(ROOT, "profiles", f"{tag}_{cfg}_{prec}_summary.txt"), "w").write(txt)
+    if traffic:
+        json.dump(traffic, open(os.path.join(ROOT, "profiles", f"traffic_{cfg}_{prec}.json"), "w"), indent=1)
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()
