@@ -21,6 +21,8 @@ named in `config`):
     --config c4   Urban3 480x640, gqmap_gpuSuper_mix_entropy L=3 K=11, 1000 its
     --config c5   RubberWhale upsampled 4x (1552x2336), column-strip tiles over
                   the ranks with RCCL ghost-column exchange (strong scaling)
+    --config c1   Dimetrodon 388x584 legacy/gqmap_cpu.m flow denoising, 50 its
+                  (device drop-in; timed call includes its host<->device copies)
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -41,7 +43,7 @@ PEAK_TFLOPS = {"fp64": 78.6, "fp32": 157.3}   # MI355X vector (non-MFMA) peaks, 
 PEAK_HBM_GBPS = 8000.0
 PAIRS = ("rubberwhale", "Dimetrodon", "Hydrangea")      # the 584x388 Middlebury pairs
 PAIRS_480 = ("Grove3", "Urban3", "Urban2", "Grove2")     # the 640x480 pairs
-DEFAULT_STEPS = {"c2": 500, "c3": 500, "c4": 1000, "c5": 100}
+DEFAULT_STEPS = {"c1": 50, "c2": 500, "c3": 500, "c4": 1000, "c5": 100}
 
 
 def algorithmic_flops_per_node(engine: str, L: int, K: int) -> float:
@@ -176,6 +178,47 @@ def run_c3(args, rank, world, local, barrier):
                          f"value counts sum over levels of level pixels x its")
 
 
+def run_c1(args, rank, world, local, barrier):
+    """legacy/gqmap_cpu.m on the GT flow of a 584x388 pair (unknowns zeroed)."""
+    from gqmap_opticalflow_amd import flow_to_color, flowio, gqmap_cpu
+    name = PAIRS[(rank + 1) % len(PAIRS)] if world > 1 else "Dimetrodon"
+    gt = flowio.load_pair(name)[2]
+    _, flo, _, unk = flow_to_color(gt, device=local)
+    o = dict(its=args.steps, K=9)
+    if args.warmup:
+        gqmap_cpu(dict(o, its=min(args.warmup, 5)), flo, seed=1, device=local)
+    barrier()
+    t0 = time.perf_counter()
+    mu, sg, rou, tr = gqmap_cpu(o, flo, seed=0, device=local, return_trace=True)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    M, N, _ = flo.shape
+    err = float(np.sqrt(((mu - flo) ** 2).sum(axis=2))[~unk].mean())
+    return dict(elapsed=elapsed, pixels=M * N, nodes=M * N, aepe=err, flow=flo, opts=o, Mo=M, No=N, its=tr.shape[0],
+                workload=f"C1: {name} {N}x{M} legacy/gqmap_cpu.m flow denoising (input = GT flow, unknowns 0), "
+                         f"K=9, var=gama=1, dta=inf, {args.steps} its, sigma0 = U+2 (seed 0); value includes the "
+                         f"call's host<->device copies; aepe = mean |mu - flow|")
+
+
+def cpu_baseline_c1(flow, opts):
+    """The C restatement of legacy/gqmap_cpu.m (single thread, as the MATLAB
+    parfor would run on one worker), bounded sample."""
+    from gqmap_opticalflow_amd import gauss_hermite
+    from oracle import oracle
+    M, N, _ = flow.shape
+    X, W = gauss_hermite(9)
+    sg0 = np.asfortranarray(np.full((M, N, 2), 2.5))
+    t0 = time.perf_counter()
+    oracle.cpu_run(dict(opts, its=1), flow, sg0, X, W)
+    t1 = time.perf_counter() - t0
+    n = max(1, min(opts["its"], int(10.0 / max(t1, 1e-3))))
+    t0 = time.perf_counter()
+    _, _, _, tr = oracle.cpu_run(dict(opts, its=n), flow, sg0, X, W)
+    dt = time.perf_counter() - t0
+    return {"value": M * N * tr.shape[0] / dt / 1e9, "unit": "Gpixel-iter/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/gqmap_legacy_oracle.c fp64, {N}x{M}, K=9, {tr.shape[0]} iterations, 1 thread, {dt:.1f}s"}
+
+
 def run_c5(args, rank, world, local, barrier, dist):
     """RubberWhale bicubic-upsampled 4x (frames with the device imresize, GT
     x4 in size and value), column-strip tiles over the ranks."""
@@ -223,7 +266,7 @@ def main():
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"))
-    ap.add_argument("--config", default="c2", choices=("c2", "c3", "c4", "c5"))
+    ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c4", "c5"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.steps is None:
@@ -259,6 +302,9 @@ def main():
     elif cfg == "c3":
         r = run_c3(args, rank, world, local, barrier)
         engine, L, K = "ctf", 1, 11
+    elif cfg == "c1":
+        r = run_c1(args, rank, world, local, barrier)
+        engine, L, K = "legacy", 1, 9
     else:
         r = run_c5(args, rank, world, local, barrier, dist)
         engine, L, K = "mixture", 1, 9
@@ -280,6 +326,9 @@ def main():
         if cfg == "c3":
             units = r["pix_its"] * world
             parallel = f"frame-parallel x{world}"
+        elif cfg == "c1":
+            units = world * r["pixels"] * r["its"]
+            parallel = f"frame-parallel x{world}"
         elif cfg == "c5":
             units = r["pixels"] * args.steps
             parallel = f"column-strip tiles x{world} (RCCL halo)"
@@ -296,7 +345,13 @@ def main():
             "config": {"workload": r["workload"], "engine": engine, "L": L, "K": K, "parallelism": parallel},
             "aepe": r["aepe"], "aepe_its": args.steps,
         }
-        if cfg == "c3":
+        if cfg == "c1":
+            # per pixel: node 2 x K x 6 flop, edges 4 x K^2 x ~40 flop (legacy/gqmap_cpu.m:20-54)
+            fl = (2 * K * 6 + 4 * K * K * 40) * r["pixels"] * r["its"]
+            out["roofline"] = {"bound": "valu", "achieved": fl / elapsed / 1e12, "peak": PEAK_TFLOPS["fp64"],
+                               "unit": "TFLOP/s", "frac": fl / elapsed / 1e12 / PEAK_TFLOPS["fp64"], "traffic": None,
+                               "kernel": "gq::k_legacy_grad + k_legacy_update (timed by the call's wall clock)"}
+        elif cfg == "c3":
             secs = elapsed
             Sb = 8 if args.precision == "fp64" else 4
             fl = algorithmic_flops_per_node("ctf", 1, K) * r["pix_its"]
@@ -311,7 +366,9 @@ def main():
             nodes = r["nodes"]
             out["roofline"] = roofline(engine, L, K, nodes, args.precision, kern_avg_s, cfg,
                                        r.get("kernel", "gq::k_iter"))
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and cfg == "c1":
+            out["cpu_baseline"] = cpu_baseline_c1(r["flow"], r["opts"])
+        elif not args.no_cpu_baseline:
             lab = {"c2": "RubberWhale", "c3": "Grove3 full-resolution level", "c4": "Urban3",
                    "c5": "RubberWhale x4"}[cfg]
             I1c, I2c, oc = r["I1"], r["I2"], r["opts"]

@@ -30,6 +30,7 @@ EXPORTS = (
     "gqmap_warp_image", "gqmap_ctf_create", "gqmap_ctf_set_images", "gqmap_ctf_run",
     "gqmap_ctf_get_level", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
     "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run",
+    "gqmap_cpu_options_default", "gqmap_cpu_run",
 )
 CTF_MAX_LEVELS = 8
 
@@ -50,6 +51,12 @@ class GqmapOptions(C.Structure):
 
 
 _D = C.POINTER(C.c_double)
+
+
+class GqmapCpuOptions(C.Structure):
+    _fields_ = [("its", C.c_int), ("K", C.c_int), ("var", C.c_double), ("gama", C.c_double),
+                ("dta", C.c_double), ("step0", C.c_double), ("step_decay", C.c_double),
+                ("corr_tor", C.c_double), ("tor", C.c_double), ("min_its", C.c_int)]
 
 
 class GqmapState(C.Structure):
@@ -117,6 +124,9 @@ def load():
         "gqmap_comm_unique_id": (C.c_int, [u8]),
         "gqmap_tile_attach_rccl": (C.c_int, [vp, u8]),
         "gqmap_tile_group_run": (C.c_int, [P(vp), C.c_int, C.c_int, P(C.c_int), _D]),
+        "gqmap_cpu_options_default": (None, [P(GqmapCpuOptions)]),
+        "gqmap_cpu_run": (C.c_int, [P(GqmapCpuOptions), _D, C.c_int, C.c_int, _D, C.c_uint64, _D, _D, _D, _D,
+                                    P(C.c_int), C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

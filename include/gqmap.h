@@ -222,6 +222,28 @@ gqmap_status gqmap_ctf_get_level(gqmap_pyramid *p, int level, int *Ml, int *Nl, 
                                  double *I2, double *flow, double *warp);
 void gqmap_ctf_destroy(gqmap_pyramid *p);
 
+/* ---- legacy flow-denoising engine: legacy/gqmap_cpu.m ----
+ * [mu,sigma,rou] = gqmap_cpu(options, flow) (legacy/gqmap_cpu.m:1): the
+ * legacy model that smooths a GIVEN flow field (Gaussian observation +
+ * truncated-quadratic pairwise terms), run on the device.  options.var /
+ * gama / dta are never set in the reference; defaults here: 1, 1, inf. */
+typedef struct gqmap_cpu_options {
+    int its, K;
+    double var, gama, dta;
+    double step0, step_decay;   /* step = step0/(1+it/step_decay): 0.1, 1000 (:62) */
+    double corr_tor;            /* rou clamp 0.97 (:65)                             */
+    double tor;                 /* stop: it > min_its && max|dmu| < tor (:70)       */
+    int min_its;                /* 100                                              */
+} gqmap_cpu_options;
+void gqmap_cpu_options_default(gqmap_cpu_options *o);
+/* flow M x N x 2 (column-major).  mu = flow; sigma = sigma0 (M x N x 2) or,
+ * when sigma0 is NULL, U(0,1) + 2 from the library RNG (seed, stream 3);
+ * rou = 0.  Outputs mu, sigma (M x N x 2), rou (M x N x 2 x 2); trace[3*i] =
+ * max|dmu|, max|dsigma|, max|drou| of iteration i+1 (its x 3, may be NULL). */
+gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int N,
+                           const double *sigma0, uint64_t seed, double *mu, double *sigma, double *rou,
+                           double *trace, int *its_done, int device);
+
 /* ---- host helpers (no device needed) ---- */
 /* imresize output length for a scale factor: ceil(scale*len). */
 int gqmap_resize_len(int len, double scale);

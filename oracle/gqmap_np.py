@@ -435,3 +435,72 @@ def ctf_pipeline(opts, img1, img2, scales, init_fn):
         warp = warp + flow
         levels.append(dict(I1w=I1w, I2=I2, flow=flow, warp=warp.copy()))
     return warp, levels
+
+
+# ---- legacy flow-denoising engine (legacy/gqmap_cpu.m), vectorised ----------
+def cpu_engine(opts, flow, sigma0, X, W):
+    """[mu, sigma, rou] = gqmap_cpu(options, flow) with sigma = sigma0 (the
+    reference draws rand(M,N,2)+2), numpy whole-array form.  Returns
+    (mu, sigma, rou, trace)."""
+    its, var, gama = int(opts["its"]), float(opts.get("var", 1.0)), float(opts.get("gama", 1.0))
+    dta = float(opts.get("dta", np.inf))
+    X, W = np.asarray(X, dtype=np.float64), np.asarray(W, dtype=np.float64)
+    XI, XJ = np.meshgrid(X, X)
+    WI, WJ = np.meshgrid(W, W)
+    WIWJ = WI * WJ
+    flow = np.asarray(flow, dtype=np.float64)
+    M, N, _ = flow.shape
+    mu, sigma = flow.copy(), np.array(sigma0, dtype=np.float64)
+    rou = np.zeros((M, N, 2, 2))
+    dnode = np.zeros((M, N, 2, 2))
+    dedge = np.zeros((M, N, 2, 5, 2))
+    S = (slice(0, M - 1), slice(0, N - 1))
+    trace = []
+    it = 1
+    while True:
+        for l in range(2):
+            x = SQRT2 * sigma[S + (l,)][..., None] * X + mu[S + (l,)][..., None]
+            dval = W * (flow[S + (l,)][..., None] - x) / var
+            dnode[S + (0, l)] = dval.sum(-1) / np.sqrt(np.pi)
+            dnode[S + (1, l)] = (dval * X).sum(-1) * np.sqrt(2 / np.pi)
+        for j in range(2):
+            S2 = (slice(1, M), slice(0, N - 1)) if j == 0 else (slice(0, M - 1), slice(1, N))
+            for l in range(2):
+                e = lambda a: a[..., None, None]
+                p = rou[S + (j, l)]
+                o1, o2 = e(sigma[S + (l,)]), e(sigma[S2 + (l,)])
+                u1, u2 = e(mu[S + (l,)]), e(mu[S2 + (l,)])
+                q, r = np.sqrt(1 + p), np.sqrt(1 - p)
+                s, t = e((q + r) / 2), e((q - r) / 2)
+                ds, dt = e((1 / q - 1 / r) / 4), e((1 / q + 1 / r) / 4)
+                ZI, ZJ = s * XI + t * XJ, t * XI + s * XJ
+                x1, x2 = SQRT2 * o1 * ZI + u1, SQRT2 * o2 * ZJ + u2
+                diff = x2 - x1
+                diff = np.where(np.abs(diff) > dta, 0.0, diff)
+                df1 = WIWJ * diff / gama
+                df2 = -df1
+                ss = lambda A: A.sum(axis=-2).sum(axis=-1)   # sum(sum(A))
+                dedge[S + (j, 0, l)] = 1 / np.pi * ss(df1)
+                dedge[S + (j, 1, l)] = 1 / np.pi * ss(df2)
+                dedge[S + (j, 2, l)] = 1 / np.pi * SQRT2 * ss(df1 * ZI)
+                dedge[S + (j, 3, l)] = 1 / np.pi * SQRT2 * ss(df2 * ZJ)
+                dedge[S + (j, 4, l)] = 1 / np.pi * SQRT2 * ss(o1 * df1 * (ds * XI + dt * XJ)
+                                                               + o2 * df2 * (dt * XI + ds * XJ))
+        z1 = np.zeros((1, N, 2))
+        z2 = np.zeros((M, 1, 2))
+        dmu = dnode[:, :, 0, :] + dedge[:, :, :, 0, :].sum(axis=2) + (
+            np.concatenate([dedge[1:, :, 0, 1, :], z1], 0) + np.concatenate([dedge[:, 1:, 1, 1, :], z2], 1))
+        dsg = dnode[:, :, 1, :] + dedge[:, :, :, 2, :].sum(axis=2) + (
+            np.concatenate([dedge[1:, :, 0, 3, :], z1], 0) + np.concatenate([dedge[:, 1:, 1, 3, :], z2], 1))
+        drou = dedge[:, :, :, 4, :]
+        step = float(opts.get("step0", 0.1)) / (1 + it / float(opts.get("step_decay", 1000.0)))
+        mu = mu + dmu * step
+        sigma = np.abs(sigma + dsg * step)
+        c = float(opts.get("corr_tor", 0.97))
+        rou = np.maximum(np.minimum(rou + drou * step, c), -c)
+        mx = np.abs(dmu).max()
+        trace.append((mx, np.abs(dsg).max(), np.abs(drou).max()))
+        it += 1
+        if it > its or (it > int(opts.get("min_its", 100)) and mx < float(opts.get("tor", 1e-3))):
+            break
+    return mu, sigma, rou, np.array(trace)

@@ -100,6 +100,22 @@ void orc_warp_image(const double *V, int M, int N, const double *warp, double *o
 /* fillmissing(A,'nearest',dim) in place */
 void orc_fillmissing_nearest(double *A, int M, int N, int dim);
 
+/* ---- legacy flow-denoising engine legacy/gqmap_cpu.m (gqmap_legacy_oracle.c) */
+typedef struct {
+    int its, K;
+    double var, gama, dta;          /* options.var / gama / dta (never set in the reference) */
+    double step0, step_decay;       /* step = 0.1/(1+it/1000) (:62)                          */
+    double corr_tor;                /* rou clamp 0.97 (:65)                                  */
+    double tor;                     /* stop: it > min_its && max|dmu| < tor (:70)            */
+    int min_its;                    /* 100                                                   */
+} orc_cpu_params;
+/* flow M x N x 2; mu/sigma (M x N x 2) and rou (M x N x 2 x 2) hold the initial
+ * state on entry (mu = flow, sigma = rand + 2, rou = 0 in the reference) and
+ * the result on exit; trace[3*i] = max|dmu|, max|dsigma|, max|drou| of
+ * iteration i+1.  Returns the number of iterations run. */
+int orc_cpu_run(const orc_cpu_params *P, const double *X, const double *W, const double *flow, int M, int N,
+                double *mu, double *sigma, double *rou, double *trace);
+
 #ifdef __cplusplus
 }
 #endif

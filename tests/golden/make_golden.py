@@ -151,8 +151,28 @@ def make_ctf_pipeline():
     print("ctf_pipeline", [lv["I1w"].shape for lv in levels], float(np.abs(warp).max()))
 
 
+# legacy flow-denoising engine (legacy/gqmap_cpu.m): Dimetrodon GT crop with
+# unknowns zeroed, sigma0 = U + 2 (seeded), var = gama = 1, dta = inf and 2.5
+def make_legacy():
+    from gqmap_opticalflow_amd.flowio import load_pair as lp
+    _, _, gt = lp("Dimetrodon")
+    flow = np.asfortranarray(gt[150:190, 200:252])
+    flow[np.abs(flow) > 1e9] = 0
+    rng = np.random.default_rng(60)
+    sigma0 = np.asfortranarray(rng.random(flow.shape) + 2)
+    X, W = gqmap_np.gauss_hermite(9)
+    out = dict(flow=flow, sigma0=sigma0, X=X, W=W)
+    for tag, dta in (("inf", np.inf), ("trunc", 2.5)):
+        opts = dict(its=12, K=9, var=1.0, gama=1.0, dta=dta)
+        mu, sg, rou, tr = gqmap_np.cpu_engine(opts, flow, sigma0, X, W)
+        out.update({f"{tag}_mu": mu, f"{tag}_sigma": sg, f"{tag}_rou": rou, f"{tag}_trace": tr})
+    np.savez_compressed(os.path.join(HERE, "legacy_cpu.npz"), **out)
+    print("legacy_cpu", flow.shape, out["inf_trace"][-1], out["trunc_trace"][-1])
+
+
 if __name__ == "__main__":
     for n, c in CASES.items():
         make_case(n, c)
     make_color()
     make_ctf_pipeline()
+    make_legacy()

@@ -1,0 +1,36 @@
+"""legacy/gqmap_cpu.m (flow-denoising QGMAP): the C restatement
+(oracle/gqmap_legacy_oracle.c) against the independent numpy restatement's
+golden (tests/golden/legacy_cpu.npz).  var/gama/dta are never set in the
+reference, so results are "parity unpinned" against MATLAB itself."""
+import os
+
+import numpy as np
+import pytest
+
+from tests import _golden as G
+
+
+def _load():
+    return dict(np.load(os.path.join(G.GOLDEN, "legacy_cpu.npz"), allow_pickle=False))
+
+
+@pytest.mark.parametrize("tag,dta", [("inf", np.inf), ("trunc", 2.5)])
+def test_legacy_oracle_matches_golden(oracle_lib, tag, dta):
+    d = _load()
+    mu, sg, rou, tr = oracle_lib.cpu_run(dict(its=12, K=9, var=1.0, gama=1.0, dta=dta), d["flow"], d["sigma0"],
+                                         d["X"], d["W"])
+    np.testing.assert_allclose(mu, d[f"{tag}_mu"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(sg, d[f"{tag}_sigma"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(rou, d[f"{tag}_rou"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(tr, d[f"{tag}_trace"], rtol=1e-12, atol=1e-12)
+
+
+def test_legacy_stop_rule_and_clamps(oracle_lib):
+    # it > 100 && max|dmu| < tor breaks the loop (legacy/gqmap_cpu.m:70); rou stays in +-0.97
+    d = _load()
+    flow = np.asfortranarray(d["flow"][:12, :14])
+    sg0 = np.asfortranarray(d["sigma0"][:12, :14])
+    X5, W5 = np.polynomial.hermite.hermgauss(5)
+    mu, sg, rou, tr = oracle_lib.cpu_run(dict(its=400, K=5, tor=1e9), flow, sg0, X5, W5)
+    assert tr.shape[0] == 100  # stops right after iteration 100
+    assert np.abs(rou).max() <= 0.97 and (sg >= 0).all()
