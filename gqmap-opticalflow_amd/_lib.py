@@ -30,7 +30,7 @@ EXPORTS = (
     "gqmap_warp_image", "gqmap_ctf_create", "gqmap_ctf_set_images", "gqmap_ctf_run",
     "gqmap_ctf_get_level", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
     "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run",
-    "gqmap_cpu_options_default", "gqmap_cpu_run",
+    "gqmap_cpu_options_default", "gqmap_cpu_run", "gqmap_read_flo", "gqmap_write_flo", "gqmap_aepe",
 )
 CTF_MAX_LEVELS = 8
 
@@ -125,6 +125,9 @@ def load():
         "gqmap_tile_attach_rccl": (C.c_int, [vp, u8]),
         "gqmap_tile_group_run": (C.c_int, [P(vp), C.c_int, C.c_int, P(C.c_int), _D]),
         "gqmap_cpu_options_default": (None, [P(GqmapCpuOptions)]),
+        "gqmap_read_flo": (C.c_int, [C.c_char_p, P(C.c_int), P(C.c_int), _D]),
+        "gqmap_write_flo": (C.c_int, [C.c_char_p, _D, C.c_int, C.c_int]),
+        "gqmap_aepe": (C.c_int, [_D, _D, u8, C.c_int, C.c_int, C.c_int, _D]),
         "gqmap_cpu_run": (C.c_int, [P(GqmapCpuOptions), _D, C.c_int, C.c_int, _D, C.c_uint64, _D, _D, _D, _D,
                                     P(C.c_int), C.c_int]),
     }

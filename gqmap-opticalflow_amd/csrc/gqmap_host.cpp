@@ -178,3 +178,105 @@ int gqmap_device_count(void)
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Middlebury .flo I/O and AEPE, host-side library calls
+// ---------------------------------------------------------------------------
+extern "C" {
+
+// readFlowFile.m:33-84: "PIEH" tag (float 202021.25), int32 width, int32
+// height, then rows of interleaved (u, v) float32; flow is M x N x 2 doubles
+// (column-major).  flow == NULL: only the size is returned.
+gqmap_status gqmap_read_flo(const char *path, int *M, int *N, double *flow)
+{
+    gq::clear_error();
+    GQ_CHECK(path && M && N, GQMAP_ERR_INVALID_ARG, "gqmap_read_flo: null argument");
+    const size_t len = std::strlen(path);
+    GQ_CHECK(len > 4 && std::strcmp(path + len - 4, ".flo") == 0, GQMAP_ERR_INVALID_ARG,
+             "readFlowFile: filename %s should have extension '.flo'", path);
+    FILE *f = std::fopen(path, "rb");
+    GQ_CHECK(f, GQMAP_ERR_INVALID_ARG, "readFlowFile: could not open %s", path);
+    float tag = 0;
+    int32_t wh[2] = {0, 0};
+    const bool hdr = std::fread(&tag, 4, 1, f) == 1 && std::fread(wh, 4, 2, f) == 2;
+    if (!hdr || tag != 202021.25f || wh[0] < 1 || wh[0] > 99999 || wh[1] < 1 || wh[1] > 99999) {
+        std::fclose(f);
+        gq::set_error("readFlowFile(%s): wrong tag or illegal size", path);
+        return GQMAP_ERR_INVALID_ARG;
+    }
+    const int W = wh[0], H = wh[1];
+    *M = H;
+    *N = W;
+    if (!flow) {
+        std::fclose(f);
+        return GQMAP_OK;
+    }
+    std::vector<float> row((size_t)2 * W);
+    for (int m = 0; m < H; ++m) {
+        if (std::fread(row.data(), sizeof(float), row.size(), f) != row.size()) {
+            std::fclose(f);
+            gq::set_error("readFlowFile(%s): truncated data", path);
+            return GQMAP_ERR_INVALID_ARG;
+        }
+        for (int n = 0; n < W; ++n) {
+            flow[m + (size_t)H * n] = row[2 * (size_t)n];
+            flow[m + (size_t)H * n + (size_t)H * W] = row[2 * (size_t)n + 1];
+        }
+    }
+    std::fclose(f);
+    return GQMAP_OK;
+}
+
+// legacy/writeFlowFile.m:33-76
+gqmap_status gqmap_write_flo(const char *path, const double *flow, int M, int N)
+{
+    gq::clear_error();
+    GQ_CHECK(path && flow && M > 0 && N > 0, GQMAP_ERR_INVALID_ARG, "gqmap_write_flo: bad argument");
+    const size_t len = std::strlen(path);
+    GQ_CHECK(len > 4 && std::strcmp(path + len - 4, ".flo") == 0, GQMAP_ERR_INVALID_ARG,
+             "writeFlowFile: filename %s should have extension '.flo'", path);
+    FILE *f = std::fopen(path, "wb");
+    GQ_CHECK(f, GQMAP_ERR_INVALID_ARG, "writeFlowFile: could not open %s", path);
+    const int32_t wh[2] = {N, M};
+    bool ok = std::fwrite("PIEH", 1, 4, f) == 4 && std::fwrite(wh, 4, 2, f) == 2;
+    std::vector<float> row((size_t)2 * N);
+    for (int m = 0; m < M && ok; ++m) {
+        for (int n = 0; n < N; ++n) {
+            row[2 * (size_t)n] = (float)flow[m + (size_t)M * n];
+            row[2 * (size_t)n + 1] = (float)flow[m + (size_t)M * n + (size_t)M * N];
+        }
+        ok = std::fwrite(row.data(), sizeof(float), row.size(), f) == row.size();
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    GQ_CHECK(ok, GQMAP_ERR_INVALID_ARG, "writeFlowFile: write to %s failed", path);
+    return GQMAP_OK;
+}
+
+// gqmap_gpu_mixture.m:63-64: flow(unknown) = 0, then
+// mean(mean(sqrt(sum((tflow - flow).^2, 3)))) over rows/cols crop..end-crop
+// (column means first).  unknown may be NULL.
+gqmap_status gqmap_aepe(const double *tflow, const double *flow, const uint8_t *unknown, int M, int N, int crop,
+                        double *out)
+{
+    gq::clear_error();
+    GQ_CHECK(tflow && flow && out, GQMAP_ERR_INVALID_ARG, "gqmap_aepe: null argument");
+    GQ_CHECK(crop >= 0 && M > 2 * crop && N > 2 * crop, GQMAP_ERR_INVALID_ARG, "gqmap_aepe: crop %d of %dx%d",
+             crop, M, N);
+    const size_t MN = (size_t)M * N;
+    double total = 0;
+    for (int n = crop; n < N - crop; ++n) {
+        double col = 0;
+        for (int m = crop; m < M - crop; ++m) {
+            const size_t q = m + (size_t)M * n;
+            const bool unk = unknown && unknown[q];
+            const double du = tflow[q] - (unk ? 0.0 : flow[q]);
+            const double dv = tflow[q + MN] - (unk ? 0.0 : flow[q + MN]);
+            col += std::sqrt(du * du + dv * dv);
+        }
+        total += col / (M - 2 * crop);
+    }
+    *out = total / (N - 2 * crop);
+    return GQMAP_OK;
+}
+
+}  // extern "C"

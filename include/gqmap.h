@@ -245,6 +245,14 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
                            double *trace, int *its_done, int device);
 
 /* ---- host helpers (no device needed) ---- */
+/* readFlowFile.m: M x N x 2 (flow == NULL: size query). */
+gqmap_status gqmap_read_flo(const char *path, int *M, int *N, double *flow);
+/* legacy/writeFlowFile.m. */
+gqmap_status gqmap_write_flo(const char *path, const double *flow, int M, int N);
+/* AEPE of gqmap_gpu_mixture.m:63-64 (unknown pixels of flow zeroed, column
+ * means over the crop..end-crop interior, then their mean); unknown may be NULL. */
+gqmap_status gqmap_aepe(const double *tflow, const double *flow, const uint8_t *unknown, int M, int N,
+                        int crop, double *out);
 /* imresize output length for a scale factor: ceil(scale*len). */
 int gqmap_resize_len(int len, double scale);
 /* GaussHermite_2(K) (GaussHermite_2.m): nodes ascending + weights. */
