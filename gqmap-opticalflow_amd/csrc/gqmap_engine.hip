@@ -72,6 +72,10 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #define GQ_STR2(x) #x
 #define GQ_PRAGMA_UNROLL(n) _Pragma(GQ_STR2(unroll n))
 #define GQ_UNROLL2 GQ_PRAGMA_UNROLL(GQ_EDGE_UNROLL_N)
+#ifndef GQ_PAIR_UNROLL_N
+#define GQ_PAIR_UNROLL_N 2
+#endif
+#define GQ_PAIR_UNROLL GQ_PRAGMA_UNROLL(GQ_PAIR_UNROLL_N)
 #define GQ_NODE_UNROLL GQ_PRAGMA_UNROLL(GQ_NODE_UNROLL_N)
 #define GQ_UNROLL_FULL _Pragma("unroll")
 #include "gqmap_math.h"
@@ -206,26 +210,18 @@ __device__ __forceinline__ fix128 load_fix_agent(const fix128 *p)
 // tot[] (LDS), all 256 threads of one workgroup.
 __device__ void fin_reduce(const FinParams &F, double *tot, fix128 *sh)
 {
-    // one pass: thread t accumulates rows t, t+256, ... of every quantity
-    // (all loads in flight together), then a wave butterfly and 4 LDS rows
+    // one quantity at a time (few live registers: this code shares the
+    // k_iter register budget when the finalize is fused)
     const int NP = NFIX + F.L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    fix128 v[NFIX + GQMAP_LMAX];
-#pragma unroll
-    for (int q = 0; q < NFIX + GQMAP_LMAX; ++q) v[q] = 0;
     const int rows = F.nranks > 0 ? F.nranks : F.nblocks;
-    for (int r = tid; r < rows; r += 256) {
-        const fix128 *row = (F.nranks > 0 ? F.gathered : F.partials) + (int64_t)r * NP;
-#pragma unroll
-        for (int q = 0; q < NFIX + GQMAP_LMAX; ++q)
-            if (q < NP) v[q] += F.nranks > 0 ? row[q] : load_fix_agent(row + q);
+    for (int q = 0; q < NP; ++q) {
+        fix128 v = 0;
+        for (int r = tid; r < rows; r += 256)
+            v += F.nranks > 0 ? F.gathered[(int64_t)r * NP + q] : load_fix_agent(F.partials + (int64_t)r * NP + q);
+        v = wave_sum_fix(v);
+        if (lane == 0) sh[q * 4 + wave] = v;
     }
-#pragma unroll
-    for (int q = 0; q < NFIX + GQMAP_LMAX; ++q)
-        if (q < NP) {
-            v[q] = wave_sum_fix(v[q]);
-            if (lane == 0) sh[q * 4 + wave] = v[q];
-        }
     __syncthreads();
     if (tid < NP) tot[tid] = from_fix((sh[tid * 4] + sh[tid * 4 + 1]) + (sh[tid * 4 + 2] + sh[tid * 4 + 3]));
     __syncthreads();

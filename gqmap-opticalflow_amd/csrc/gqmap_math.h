@@ -314,7 +314,35 @@ struct Sums {
         sm = fma(tab[6 * TAB_STRIDE + k], f, sm);
         sx = fma(tab[7 * TAB_STRIDE + k], f, sx);
     }
+    // point k and its mirror K^2-1-k (xi, xj -> -xi, -xj: the Gauss-Hermite
+    // rule is symmetric, so w, w(xi^2+-xj^2), w xi xj are shared and w xi,
+    // w xj change sign): fp = f(k), fm = f(mirror)
+    template <typename TP>
+    GQ_HD void add_pair(TP tab, int k, R fp, R fm)
+    {
+        const R fs = fp + fm, fd = fp - fm;
+        s0 = fma(tab[2 * TAB_STRIDE + k], fs, s0);
+        sxi = fma(tab[3 * TAB_STRIDE + k], fd, sxi);
+        sxj = fma(tab[4 * TAB_STRIDE + k], fd, sxj);
+        sa = fma(tab[5 * TAB_STRIDE + k], fs, sa);
+        sm = fma(tab[6 * TAB_STRIDE + k], fs, sm);
+        sx = fma(tab[7 * TAB_STRIDE + k], fs, sx);
+    }
 };
+
+// Quadrature loop order shared by the node and edge sums.  The K x K
+// points come in mirror pairs (k, K^2-1-k), k < K^2/2, plus the centre
+// (k = (K^2-1)/2, xi = xj = 0) when K is odd.  Lane j of Q takes the pairs
+// k = j, j+Q, ... in increasing k and, if (npairs - j) % Q == 0, the centre
+// last.  body_pair(k) / body_center(k) do the evaluation and accumulation.
+template <typename FP, typename FC>
+GQ_HD void quad_pairs(int k0, int K2, int dk, FP body_pair, FC body_center)
+{
+    const int np = K2 >> 1;
+    GQ_PAIR_UNROLL
+    for (int k = k0; k < np; k += dk) body_pair(k);
+    if ((K2 & 1) && np >= k0 && (np - k0) % dk == 0) body_center(np);
+}
 
 template <typename R>
 GQ_HD void spectral_st(R p, R &s, R &t)
@@ -404,11 +432,18 @@ template <typename R, typename TP>
 GQ_HD Sums<R> edge_sums(TP tab, int k0, int K2, int dk, R eps, const EdgeCoef<R> &c)
 {
     Sums<R> S;
-    GQ_UNROLL2
-    for (int k = k0; k < K2; k += dk) {
-        const R d = fma(c.A, tab[k], fma(c.B, tab[TAB_STRIDE + k], c.C));
-        S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
-    }
+    quad_pairs(
+        k0, K2, dk,
+        [&](int k) {
+            // d = C +- p with p = A xi + B xj
+            const R p = fma(c.A, tab[k], c.B * tab[TAB_STRIDE + k]);
+            const R dp = c.C + p, dm = c.C - p;
+            S.add_pair(tab, k, GQ_SQRT(fma(dp, dp, eps)), GQ_SQRT(fma(dm, dm, eps)));
+        },
+        [&](int k) {
+            const R d = fma(c.A, tab[k], fma(c.B, tab[TAB_STRIDE + k], c.C));
+            S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+        });
     return S;
 }
 template <typename R>
@@ -449,20 +484,26 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
     Sums<R> S;
     if (ENG != 1) {
         const R I = I1[m + (int64_t)Mo * n];
+        auto f_at = [&](R x1, R x2) {
+            const R v = ENG == 2 ? sample_ctf(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
+                                 : sample(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
+            const R d = I - v;
+            return GQ_SQRT(fma(d, d, eps));
+        };
+        // one point at a time in increasing k (mirror pairs sample far-apart
+        // cells: measured slower for the gathers, unlike the edge sums)
         GQ_NODE_UNROLL
         for (int k = k0; k < K2; k += dk) {
             const R x1 = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], u1));
             const R x2 = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], u2));
-            const R v = ENG == 2 ? sample_ctf(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
-                                 : sample(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
-            const R d = I - v;
-            S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+            S.add(tab, k, f_at(x1, x2));
         }
     } else {
         // super = sum_{i=top..bottom} sum_{j=left..right} node_pot(x1,x2,i,j): j fastest
         R I[16];
         const int i0 = 4 * m, j0 = 4 * n;  // 0-based top-left pixel of the block
         for (int q = 0; q < 16; ++q) I[q] = I1[(i0 + (q >> 2)) + (int64_t)Mo * (j0 + (q & 3))];
+        // (one point at a time: a pair of 4x4 block sums costs more VGPRs than it saves)
         for (int k = k0; k < K2; k += dk) {
             const R x1 = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], u1));
             const R x2 = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], u2));
