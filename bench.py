@@ -224,7 +224,10 @@ def run_c5(args, rank, world, local, barrier, dist):
     x4 in size and value), column-strip tiles over the ranks."""
     from gqmap_opticalflow_amd import Engine, aepe, comm_unique_id, flow_to_color, flowio, imresize
     I1s, I2s, gt = flowio.load_pair("rubberwhale")
-    I1, I2 = imresize(I1s, 4.0, device=local), imresize(I2s, 4.0, device=local)
+    # imresize of the uint8 frames as the drivers do (imresize(imread(..),scale),
+    # optical_flowSuper.m:8-9): round half away from zero and saturate to uint8
+    u8 = lambda a: np.asfortranarray(np.clip(np.sign(a) * np.floor(np.abs(a) + 0.5), 0, 255))
+    I1, I2 = u8(imresize(I1s, 4.0, device=local)), u8(imresize(I2s, 4.0, device=local))
     # GT x4 in value (unknown entries stay > 1e9) and in size (nearest)
     gt4 = np.asfortranarray(np.repeat(np.repeat(gt * 4.0, 4, axis=0), 4, axis=1))
     _, flo, (minu, maxu, minv, maxv), unk = flow_to_color(gt4, device=local)
@@ -255,7 +258,8 @@ def run_c5(args, rank, world, local, barrier, dist):
     e = np.sqrt(((flo[sl] - f[sl]) ** 2).sum(axis=2))
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, pixels=Mo * No, nodes=Mo * (col1 - col0),
                 err_sum=float(e.sum()), err_n=int(e.size), Mo=Mo, No=No, I1=I1, I2=I2, opts=opts,
-                workload=f"C5: RubberWhale upsampled 4x ({No}x{Mo}, bicubic), mixture L=1 K=9, "
+                workload=f"C5: RubberWhale upsampled 4x ({No}x{Mo}, bicubic imresize, uint8-rounded as "
+                         f"imresize(imread(..)) gives), mixture L=1 K=9, "
                          f"{world} column-strip tile(s), RCCL ghost-column + totals exchange per iteration, "
                          f"its={args.steps}")
 

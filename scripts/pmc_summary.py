@@ -55,7 +55,7 @@ def main():
     wcorr = GiB / (f_write * 1024) if f_write else None
     out_stats = os.path.join(ROOT, "profiles", f"{tag}_{cfg}_{prec}_kernel_stats.csv")
     shutil.copy(stats, out_stats)
-    lines = [f"profile {tag} config {cfg} precision {prec} (bench.py --steps 200 --warmup 5 under rocprofv3)",
+    lines = [f"profile {tag} config {cfg} precision {prec} (bench.py --warmup 5 under rocprofv3; steps in the .log)",
              f"calibration ({width} lanes, 1 GiB): FETCH_SIZE x{fcorr:.3f}, WRITE_SIZE x{wcorr:.3f}"
              if fcorr and wcorr else "calibration: missing", ""]
     lines.append(f"{'kernel':70s} {'calls':>6s} {'avg_us':>10s} {'FETCH_KB':>12s} {'WRITE_KB':>12s} {'HBM_MB(corr)':>13s}")
