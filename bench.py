@@ -281,10 +281,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # GQMAP_BENCH_BACKEND=gloo rehearses the multi-rank harness on a box with
+    # fewer GPUs than ranks (ranks then share devices round-robin); the
+    # driver's runs use RCCL ("nccl") with one GPU per rank.
+    backend = os.environ.get("GQMAP_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
         local = 0
@@ -316,11 +324,12 @@ def main():
     elapsed = r["elapsed"]
     kernel_ms = r.get("kernel_ms", 0.0)
     if dist is not None:
-        t = torch.tensor([elapsed, kernel_ms], device="cuda", dtype=torch.float64)
+        dev = "cuda" if backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = t.tolist()
         if cfg == "c5":
-            s = torch.tensor([r["err_sum"], r["err_n"]], device="cuda", dtype=torch.float64)
+            s = torch.tensor([r["err_sum"], r["err_n"]], device=dev, dtype=torch.float64)
             dist.all_reduce(s)
             r["aepe"] = s[0].item() / s[1].item()
     elif cfg == "c5":
