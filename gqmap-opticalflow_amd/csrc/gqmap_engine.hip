@@ -135,6 +135,7 @@ struct IterParams {
     // fused finalize: the last workgroup to finish (arrival ticket in Ctl)
     // reduces the partials and runs the k_finalize step in the same launch
     int fused;
+    int cu_group, cu_slots;  // co-resident workgroups per CU, CUs per XCD (tile order only)
     FinParams fin;
     R epsn, lamd, lams;
     R minu, maxu, minv, maxv, sig_lo, sig_hi, corr, sig_step;
@@ -314,6 +315,20 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     const int nb = P.tiles_m * P.tiles_n;
     const int b = blockIdx.x;
     int tile = b >> 3;
+    // Within an XCD, local blocks j, j+S, j+2S, ... (S = CUs per XCD) start on
+    // the same CU (scripts/micro/placement.hip): give those co-resident blocks
+    // vertically adjacent tiles of the band (shared L1 lines of the gathers).
+    if (P.cu_group > 1) {
+        const int band = (nb - (b & 7) + 7) >> 3, S = P.cu_slots;
+        if (P.cu_group >= 100) {  // whole band: slot s takes a contiguous run
+            const int Rn = (band + S - 1) / S, X = band - (Rn - 1) * S;  // X slots get Rn tiles
+            const int s = tile % S, r = tile / S;
+            tile = s * (Rn - 1) + min(s, X) + r;
+        } else {
+            const int g = min(P.cu_group, band / S);
+            if (g > 1 && tile < S * g) tile = (tile % S) * g + tile / S;
+        }
+    }
     {
         const int xcd = b & 7;
         for (int y = 0; y < xcd; ++y) tile += (nb - y + 7) >> 3;
@@ -743,6 +758,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.n_off = c->n_off; P.own_lo = c->own_lo; P.own_hi = c->own_hi; P.Ng = c->Ng;
     P.fused = fused_finalize(c);
     P.fin = fin_params(c);
+    P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     return P;
 }
 
@@ -764,15 +780,38 @@ FinParams fin_params(const gqmap_ctx *c)
     return F;
 }
 
+// Resident workgroups per CU for a k_iter instantiation, and CUs per XCD:
+// the tile grouping of k_iter (speed only, never results).
+template <typename R, typename VT, int ENG, int Q>
+void launch_k_iter(gqmap_ctx *c)
+{
+    static const int2 shape = [] {
+        int per_cu = 1, dev = 0, cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_iter<R, VT, ENG, Q>, BLOCK, 0) != hipSuccess)
+            per_cu = 1;
+        if (hipGetDevice(&dev) == hipSuccess)
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return make_int2(std::max(1, per_cu), std::max(1, cus / 8));
+    }();
+    IterParams<R, VT> P = iter_params<R, VT>(c);
+    if (!getenv("GQMAP_NO_CU_GROUP")) {
+        P.cu_group = shape.x;
+        P.cu_slots = shape.y;
+        if (const char *g = getenv("GQMAP_CU_GROUP")) P.cu_group = atoi(g);
+        if (getenv("GQMAP_CU_GROUP_PRINT")) fprintf(stderr, "k_iter Q=%d cu_group %d cu_slots %d\n", Q, P.cu_group, P.cu_slots);
+    }
+    k_iter<R, VT, ENG, Q><<<c->nblocks, BLOCK, 0, c->stream>>>(P);
+}
+
 template <typename R, typename VT, int ENG>
 void launch_iter_q(gqmap_ctx *c)
 {
     if (c->split == 16)
-        k_iter<R, VT, ENG, 16><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+        launch_k_iter<R, VT, ENG, 16>(c);
     else if (c->split == 4)
-        k_iter<R, VT, ENG, 4><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+        launch_k_iter<R, VT, ENG, 4>(c);
     else
-        k_iter<R, VT, ENG, 1><<<c->nblocks, BLOCK, 0, c->stream>>>(iter_params<R, VT>(c));
+        launch_k_iter<R, VT, ENG, 1>(c);
 }
 
 template <typename R, typename VT>
