@@ -66,6 +66,9 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #ifndef GQ_NODE_UNROLL_N
 #define GQ_NODE_UNROLL_N 1
 #endif
+#ifndef GQ_PHASE_MIX
+#define GQ_PHASE_MIX 1
+#endif
 #ifndef GQ_MIN_WAVES
 #define GQ_MIN_WAVES 1
 #endif
@@ -359,6 +362,9 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     fix128 fE = 0, fmu = 0, fsg = 0;
     int nonfinite = 0;
     const int wave = tid >> 6, lane = tid & 63;
+    // workgroups that start on one CU are local blocks j, j+S, j+2S of the
+    // XCD (see the tile order above): alternate the phase order among them
+    const bool edge_first = GQ_PHASE_MIX && (((b >> 3) / P.cu_slots) & 1);
     // halo: 4*TM edges (top row and left column, u and v) x Q lanes, whole waves
     constexpr int HALO_LANES = 4 * TM * Q;
     const bool halo_lane = tid < HALO_LANES;
@@ -370,6 +376,15 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
 #pragma unroll
         for (int q = 0; q < NPLANES; ++q) own[q] = valid ? src[i + MNL * q] : R(0);
         Grad<R> nd{};
+        R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
+        R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
+        R eE = 0, eda = 0;                                     // sum over the 4 edges
+        // Two phases, node then edges or (edge_first) edges then node: the
+        // node phase is gather-heavy, the edge phase pure VALU, and mixing the
+        // orders among the workgroups that share a CU overlaps the two.
+#pragma unroll 1
+        for (int ph = 0; ph < 2; ++ph) {
+        if ((ph == 0) != edge_first) {
         if (inner) {
             const NodeCoef<R> c = node_coef(own[2], own[3], own[4]);
             Sums<R> S = node_sums<ENG>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
@@ -377,13 +392,11 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
             if (Q > 1) S = lane_combine<Q>(S);
             nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, own[2], own[3], own[4], ENG == 2);
         }
+        } else {
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
         // edges, then job 4 on the halo lanes: the edges entering the tile from
         // the row above / the column to the left.  One edge body, streamed into
         // accumulators and LDS, keeps VGPRs low.
-        R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
-        R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
-        R eE = 0, eda = 0;                                     // sum over the 4 edges
         const int njobs = halo_lane ? 5 : 4;  // wave-uniform
 #pragma unroll 1
         for (int e = 0; e < njobs; ++e) {
@@ -432,6 +445,8 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
                 if (dir == 0) { in_up[uv][0][hr * TM] = g.du2; in_up[uv][1][hr * TM] = g.do2; }
                 else          { in_left[uv][0][hr] = g.du2; in_left[uv][1][hr] = g.do2; }
             }
+        }
+        }
         }
         __syncthreads();
         fix128 fda = 0;
