@@ -66,6 +66,12 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #ifndef GQ_NODE_UNROLL_N
 #define GQ_NODE_UNROLL_N 1
 #endif
+#ifndef GQ_PIPE_FENCES  // 1: release/acquire fences around tile hand-offs; 0: sc1 stores + sc1 loads
+#define GQ_PIPE_FENCES 0
+#endif
+#ifndef GQ_PIPE_STATS  // instrumentation builds only: dependency-wait / busy cycles of the pipelined kernel
+#define GQ_PIPE_STATS 0
+#endif
 #ifndef GQ_PHASE_MIX
 #define GQ_PHASE_MIX 1
 #endif
@@ -99,6 +105,13 @@ struct Ctl {
     int done;  // completed iterations since the state was set (ping-pong parity)
     int stop;  // ptdmu < tor reached
     int arrive;  // fused finalize: workgroups done with this iteration
+    // pipelined kernel (k_iter_pipe): work queue, the launch's first
+    // iteration and completed count, last finalized iteration, arrival
+    // tickets of the two iterations in flight
+    int queue, launch_it, launch_done, fin_it;
+    int arrive2[2];
+    // GQ_PIPE_STATS builds: cycles spent waiting for dependencies / in tiles, items
+    unsigned long long st_wait, st_busy, st_items;
     double T;
     double alpha[GQMAP_LMAX];
     double w[GQMAP_LMAX];
@@ -297,45 +310,99 @@ __device__ void fin_apply(const FinParams &F, const double *tot)
 // Lane j of a node sums the quadrature points k = j, j+Q, ... and the lanes
 // combine with an xor butterfly (the spec's butterfly()).
 // ---------------------------------------------------------------------------
-template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> P)
+// Tile index of block b: XCD-aware order.  Blocks b and b+8 share an XCD
+// (round-robin dispatch), so each XCD gets a contiguous band of tiles (L2
+// locality of the VV gathers).  Speed only; results never depend on placement.
+__device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
+{
+    int tile = b >> 3;
+    // Within an XCD, local blocks j, j+S, j+2S, ... (S = CUs per XCD) start on
+    // the same CU (scripts/micro/placement.hip): give those co-resident blocks
+    // vertically adjacent tiles of the band (shared L1 lines of the gathers).
+    if (cu_group > 1) {
+        const int band = (nb - (b & 7) + 7) >> 3;
+        if (cu_group >= 100) {  // whole band: slot s takes a contiguous run
+            const int Rn = (band + S - 1) / S, X = band - (Rn - 1) * S;  // X slots get Rn tiles
+            const int s = tile % S, r = tile / S;
+            tile = s * (Rn - 1) + min(s, X) + r;
+        } else {
+            const int g = min(cu_group, band / S);
+            if (g > 1 && tile < S * g) tile = (tile % S) * g + tile / S;
+        }
+    }
+    const int xcd = b & 7;
+    for (int y = 0; y < xcd; ++y) tile += (nb - y + 7) >> 3;
+    return tile;
+}
+
+// State store of the update: plain, or (PIPE) a device-coherent write-through
+// store -- the pipelined kernel hands tiles to other workgroups in-launch.
+template <bool PIPE, typename R>
+__device__ __forceinline__ void put_state(R *p, R v)
+{
+    if (PIPE) {
+        if (sizeof(R) == 8) {
+            uint64_t u;
+            __builtin_memcpy(&u, &v, 8);
+            __hip_atomic_store(reinterpret_cast<uint64_t *>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            uint32_t u;
+            __builtin_memcpy(&u, &v, 4);
+            __hip_atomic_store(reinterpret_cast<uint32_t *>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        *p = v;
+    }
+}
+
+// State load: plain, or (PIPE without fences) a device-coherent sc1 load.
+template <bool PIPE, typename R>
+__device__ __forceinline__ R get_state(const R *p)
+{
+    if (PIPE && !GQ_PIPE_FENCES) {
+        if (sizeof(R) == 8) {
+            const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            R v;
+            __builtin_memcpy(&v, &u, 8);
+            return v;
+        } else {
+            const uint32_t u = __hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            R v;
+            __builtin_memcpy(&v, &u, 4);
+            return v;
+        }
+    }
+    return *p;
+}
+
+// LDS of one tile: in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n);
+// in_left: from (m,n-1); red: per-wave partial sums.  Declared by the kernels
+// (one copy whatever the number of iter_tile instantiations).
+template <typename R, int TPIX>
+struct TileLds {
+    R in_up[2][2][TPIX];
+    R in_left[2][2][TPIX];
+    fix128 red[GQMAP_LMAX + NFIX][4];
+};
+
+// One tile of one iteration (absolute iteration `it`, reading state buffer
+// `parity`): node and edge gradients, neighbour scatter, clamped ascent into
+// the other buffer, and the tile's exact partial sums into part_row[0..NP).
+template <typename R, typename VT, int ENG, int Q, bool PIPE, bool EDGE_FIRST>
+__device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, int it, int parity,
+                                          fix128 *part_row, TileLds<R, BLOCK / Q> &lds)
 {
     constexpr int TPIX = BLOCK / Q;                   // nodes per tile
     constexpr int TM = Q == 1 ? 16 : Q == 4 ? 8 : 4;  // tile side
     static_assert(TM * TM == TPIX, "tile");
     Ctl *ctl = P.ctl;
-    if (ctl->stop) return;
-    const int it = ctl->it;
-    const int parity = ctl->done & 1;
     const R *__restrict__ src = parity ? P.st1 : P.st0;
     R *__restrict__ dst = parity ? P.st0 : P.st1;
     const R T = R(ctl->T);
     const R step = R(P.step0 / (1.0 + it / P.step_decay));
 
-    // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin
-    // dispatch), so each XCD gets a contiguous band of tiles (L2 locality of
-    // the VV gathers).  Speed only; results never depend on placement.
-    const int nb = P.tiles_m * P.tiles_n;
-    const int b = blockIdx.x;
-    int tile = b >> 3;
-    // Within an XCD, local blocks j, j+S, j+2S, ... (S = CUs per XCD) start on
-    // the same CU (scripts/micro/placement.hip): give those co-resident blocks
-    // vertically adjacent tiles of the band (shared L1 lines of the gathers).
-    if (P.cu_group > 1) {
-        const int band = (nb - (b & 7) + 7) >> 3, S = P.cu_slots;
-        if (P.cu_group >= 100) {  // whole band: slot s takes a contiguous run
-            const int Rn = (band + S - 1) / S, X = band - (Rn - 1) * S;  // X slots get Rn tiles
-            const int s = tile % S, r = tile / S;
-            tile = s * (Rn - 1) + min(s, X) + r;
-        } else {
-            const int g = min(P.cu_group, band / S);
-            if (g > 1 && tile < S * g) tile = (tile % S) * g + tile / S;
-        }
-    }
-    {
-        const int xcd = b & 7;
-        for (int y = 0; y < xcd; ++y) tile += (nb - y + 7) >> 3;
-    }
     const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
     const int tid = threadIdx.x;
     const int pix = tid / Q, kj = tid % Q;  // node within the tile, lane within the node
@@ -354,17 +421,13 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     const ctab_t<R> tab = as_const(P.tab);
     const int K2 = P.K2;
 
-    // in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n); in_left: from (m,n-1)
-    __shared__ R in_up[2][2][TPIX];
-    __shared__ R in_left[2][2][TPIX];
-    __shared__ fix128 red[GQMAP_LMAX + NFIX][4];
+    auto &in_up = lds.in_up;
+    auto &in_left = lds.in_left;
+    auto &red = lds.red;
 
     fix128 fE = 0, fmu = 0, fsg = 0;
     int nonfinite = 0;
     const int wave = tid >> 6, lane = tid & 63;
-    // workgroups that start on one CU are local blocks j, j+S, j+2S of the
-    // XCD (see the tile order above): alternate the phase order among them
-    const bool edge_first = GQ_PHASE_MIX && (((b >> 3) / P.cu_slots) & 1);
     // halo: 4*TM edges (top row and left column, u and v) x Q lanes, whole waves
     constexpr int HALO_LANES = 4 * TM * Q;
     const bool halo_lane = tid < HALO_LANES;
@@ -374,17 +437,12 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
         const int64_t i = m + (int64_t)M * n + MN * l;
         R own[NPLANES];
 #pragma unroll
-        for (int q = 0; q < NPLANES; ++q) own[q] = valid ? src[i + MNL * q] : R(0);
+        for (int q = 0; q < NPLANES; ++q) own[q] = valid ? get_state<PIPE>(&src[i + MNL * q]) : R(0);
         Grad<R> nd{};
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
         R eE = 0, eda = 0;                                     // sum over the 4 edges
-        // Two phases, node then edges or (edge_first) edges then node: the
-        // node phase is gather-heavy, the edge phase pure VALU, and mixing the
-        // orders among the workgroups that share a CU overlaps the two.
-#pragma unroll 1
-        for (int ph = 0; ph < 2; ++ph) {
-        if ((ph == 0) != edge_first) {
+        auto node_phase = [&]() {
         if (inner) {
             const NodeCoef<R> c = node_coef(own[2], own[3], own[4]);
             Sums<R> S = node_sums<ENG>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
@@ -392,7 +450,8 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
             if (Q > 1) S = lane_combine<Q>(S);
             nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, own[2], own[3], own[4], ENG == 2);
         }
-        } else {
+        };
+        auto edge_phase = [&]() {
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
         // edges, then job 4 on the halo lanes: the edges entering the tile from
         // the row above / the column to the left.  One edge body, streamed into
@@ -421,12 +480,12 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
             if (need) {
                 const int64_t h = hm + (int64_t)M * hn + MN * l;
                 const int64_t r = rm + (int64_t)M * rn + MN * l;
-                const R u1 = own_edge ? (uv ? own[1] : own[0]) : src[h + MNL * uv];
-                const R o1 = own_edge ? (uv ? own[3] : own[2]) : src[h + MNL * (2 + uv)];
+                const R u1 = own_edge ? (uv ? own[1] : own[0]) : get_state<PIPE>(&src[h + MNL * uv]);
+                const R o1 = own_edge ? (uv ? own[3] : own[2]) : get_state<PIPE>(&src[h + MNL * (2 + uv)]);
                 const R p = own_edge ? (e == 0 ? own[5] : e == 1 ? own[6] : e == 2 ? own[7] : own[8])
-                                     : src[h + MNL * (5 + dir + 2 * uv)];
-                const R o2 = src[r + MNL * (2 + uv)];
-                const EdgeCoef<R> c = edge_coef(u1, src[r + MNL * uv], o1, o2, p);
+                                     : get_state<PIPE>(&src[h + MNL * (5 + dir + 2 * uv)]);
+                const R o2 = get_state<PIPE>(&src[r + MNL * (2 + uv)]);
+                const EdgeCoef<R> c = edge_coef(u1, get_state<PIPE>(&src[r + MNL * uv]), o1, o2, p);
                 Sums<R> S = edge_sums(tab, kj, K2, Q, P.epsn, c);
                 if (Q > 1) S = lane_combine<Q>(S);
                 g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p, ENG == 2);
@@ -446,7 +505,17 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
                 else          { in_left[uv][0][hr] = g.du2; in_left[uv][1][hr] = g.do2; }
             }
         }
-        }
+        };
+        // Node phase then edge phase, or (EDGE_FIRST) the reverse: the node
+        // phase is gather-heavy, the edge phase pure VALU; mixing the orders
+        // among the workgroups that share a CU overlaps the two.  Each order
+        // is its own straight-line instantiation (registers allocated alone).
+        if (EDGE_FIRST) {
+            edge_phase();
+            node_phase();
+        } else {
+            node_phase();
+            edge_phase();
         }
         __syncthreads();
         fix128 fda = 0;
@@ -457,18 +526,18 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
             const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][pix]) + in_left[0][1][pix];
             const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
-            dst[i + MNL * 0] = cl(own[0] + gmu_u * step, P.minu, P.maxu);
-            dst[i + MNL * 1] = cl(own[1] + gmu_v * step, P.minv, P.maxv);
+            put_state<PIPE, R>(&dst[i + MNL * 0], cl(own[0] + gmu_u * step, P.minu, P.maxu));
+            put_state<PIPE, R>(&dst[i + MNL * 1], cl(own[1] + gmu_v * step, P.minv, P.maxv));
             // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
             const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
             const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
-            dst[i + MNL * 2] = cl(own[2] + su, P.sig_lo, P.sig_hi);
-            dst[i + MNL * 3] = cl(own[3] + sv, P.sig_lo, P.sig_hi);
-            dst[i + MNL * 4] = cl(own[4] + nd.dp * step, -P.corr, P.corr);
-            dst[i + MNL * 5] = cl(own[5] + drou0 * step, -P.corr, P.corr);
-            dst[i + MNL * 6] = cl(own[6] + drou1 * step, -P.corr, P.corr);
-            dst[i + MNL * 7] = cl(own[7] + drou2 * step, -P.corr, P.corr);
-            dst[i + MNL * 8] = cl(own[8] + drou3 * step, -P.corr, P.corr);
+            put_state<PIPE, R>(&dst[i + MNL * 2], cl(own[2] + su, P.sig_lo, P.sig_hi));
+            put_state<PIPE, R>(&dst[i + MNL * 3], cl(own[3] + sv, P.sig_lo, P.sig_hi));
+            put_state<PIPE, R>(&dst[i + MNL * 4], cl(own[4] + nd.dp * step, -P.corr, P.corr));
+            put_state<PIPE, R>(&dst[i + MNL * 5], cl(own[5] + drou0 * step, -P.corr, P.corr));
+            put_state<PIPE, R>(&dst[i + MNL * 6], cl(own[6] + drou1 * step, -P.corr, P.corr));
+            put_state<PIPE, R>(&dst[i + MNL * 7], cl(own[7] + drou2 * step, -P.corr, P.corr));
+            put_state<PIPE, R>(&dst[i + MNL * 8], cl(own[8] + drou3 * step, -P.corr, P.corr));
             // per-node contributions to the global sums (exact fixed point)
             const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
             const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
@@ -501,9 +570,29 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     if (tid < NP) {  // NP <= 12: all in wave 0
         fix128 v = 0;
         if (tid < NFIX || P.L > 1) v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        store_fix_agent(&P.partials[(int64_t)blockIdx.x * NP + tid], v);
+        store_fix_agent(&part_row[tid], v);
     }
+}
+
+template <typename R, typename VT, int ENG, int Q>
+__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> P)
+{
+    Ctl *ctl = P.ctl;
+    if (ctl->stop) return;
+    const int nb = P.tiles_m * P.tiles_n;
+    const int b = blockIdx.x;
+    const int tile = tile_of_block(b, nb, P.cu_group, P.cu_slots);
+    // workgroups that start on one CU are local blocks j, j+S, j+2S of the
+    // XCD (see tile_of_block): alternate the phase order among them
+    const bool edge_first = GQ_PHASE_MIX && (((b >> 3) / P.cu_slots) & 1);
+    const int NP = NFIX + P.L;
+    __shared__ TileLds<R, BLOCK / Q> lds;
+    if (edge_first)
+        iter_tile<R, VT, ENG, Q, false, true>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds);
+    else
+        iter_tile<R, VT, ENG, Q, false, false>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds);
     if (!P.fused) return;
+    const int tid = threadIdx.x;
     // Last workgroup in runs the finalize step: release the partials at
     // device scope (the XCDs' L2s are not coherent), take an arrival ticket,
     // and the final arriver acquires them all.
@@ -524,6 +613,181 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     if (tid == 0) {
         fin_apply(P.fin, tot);
         ctl->arrive = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// pipelined iteration kernel
+//
+// One launch runs n_iter iterations.  Its workgroups take items (iteration j,
+// tile) from one device-wide queue in (j, tile) order; an item waits only for
+// the tiles it reads -- itself and its 4 neighbour tiles -- to have finished
+// iteration j-1 (per-tile counters), so iteration j+1 starts on one part of
+// the frame while iteration j drains elsewhere: no per-launch fill and drain,
+// no tail.  The update is Jacobi with two state buffers, and a tile of
+// iteration j+1 overwrites buffer (j+1)&1 = (j-1)&1 only after its neighbours
+// finished reading it in iteration j (the same counters).  Partial sums go to
+// one of two slots (j&1); the last tile of iteration j runs its finalize
+// after that of j-1.  Items of iteration j wait for the finalize of j-2: a
+// stop (ptdmu < tor) at iteration s lets at most iteration s+1 run
+// speculatively, into the buffer that held s-1, and is then discarded --
+// the state of iteration s stays intact.  Used when nothing the items read
+// changes between iterations (L = 1, constant temperature): alpha, T and the
+// step (a function of it) are then fixed per item.
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): state and
+// partials are stored write-through (sc1); every wave drains its stores,
+// the workgroup meets at a barrier, lane 0 releases at agent scope and then
+// publishes the tile counter / takes the arrival ticket; a consumer polls
+// with sc1 loads, acquires at agent scope, and its waves pass a barrier
+// before reading.  The queue is only popped by running workgroups, so an
+// item never waits for one that has not been handed out: no deadlock for any
+// grid size or residency.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int ld_agent(const int *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(int *p, int v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Spin until *p >= v; false if the run stopped meanwhile (a stop at
+// iteration s is set after every item of s completed, so whoever still waits
+// belongs to a discarded iteration > s).
+__device__ __forceinline__ bool wait_ge(const int *p, int v, const int *stop)
+{
+    while (ld_agent(p) < v) {
+        if (ld_agent(stop)) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+// Before each pipelined launch (all earlier work is complete at a launch
+// boundary): reset the queue and tickets, every tile counter and the
+// finalize counter to "iteration it-1 done".
+__global__ void k_pipe_prep(Ctl *ctl, int *done_it, int nb)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int it = ctl->it;
+    if (i < nb) done_it[i] = it - 1;
+    if (i == 0) {
+        ctl->queue = 0;
+        ctl->arrive2[0] = ctl->arrive2[1] = 0;
+        ctl->launch_it = it;
+        ctl->launch_done = ctl->done;
+        ctl->fin_it = it - 1;
+        ctl->st_wait = ctl->st_busy = ctl->st_items = 0;
+    }
+}
+
+// The finalizer workgroup of the pipelined kernel (block 0: dispatched
+// first, so it is resident whatever the residency of the grid): iteration by
+// iteration, wait until every tile has arrived, reduce the partials, apply
+// the finalize step, re-arm the ticket and publish fin_it.  A workgroup of
+// its own keeps this code out of the item loop (inlined there it raised the
+// loop's register allocation by a wave per SIMD).
+__device__ void pipe_finalizer(const FinParams &F0, fix128 *partials, int nb, int NP, int it0, int n_iter,
+                               double *tot, fix128 *sh_red, int *sh_ok)
+{
+    Ctl *ctl = F0.ctl;
+    const int tid = threadIdx.x;
+    for (int j = 0; j < n_iter; ++j) {
+        const int it = it0 + j;
+        if (tid == 0) {
+            // stop is only ever set by this loop: no wait can miss it
+            *sh_ok = !ld_agent(&ctl->stop) && wait_ge(&ctl->arrive2[it & 1], nb, &ctl->stop);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (!*sh_ok) return;
+        FinParams F = F0;
+        F.partials = partials + (int64_t)(it & 1) * nb * NP;
+        F.nblocks = nb;
+        fin_reduce(F, tot, sh_red);
+        if (tid == 0) {
+            fin_apply(F, tot);
+            st_agent(&ctl->arrive2[it & 1], 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st_agent(&ctl->fin_it, it);
+        }
+        __syncthreads();
+    }
+}
+
+template <typename R, typename VT, int ENG, int Q>
+__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter_pipe(IterParams<R, VT> P, int n_iter,
+                                                                   int *done_it)
+{
+    Ctl *ctl = P.ctl;
+    const int nb = P.tiles_m * P.tiles_n;
+    const int NP = NFIX + P.L;
+    const int tid = threadIdx.x;
+    const int it0 = ctl->launch_it, done0 = ctl->launch_done;  // set by k_pipe_prep
+    const int64_t items = (int64_t)n_iter * nb;
+    __shared__ int sh_item;
+    __shared__ TileLds<R, BLOCK / Q> lds;
+    if (blockIdx.x == 0) {
+        __shared__ double tot[NFIX + GQMAP_LMAX];
+        __shared__ fix128 sh_red[256];
+        pipe_finalizer(P.fin, P.partials, nb, NP, it0, n_iter, tot, sh_red, &sh_item);
+        return;
+    }
+    for (int k = 0;; ++k) {
+#if GQ_PIPE_STATS
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (tid == 0) {
+            int item = -1;
+            const int q = atomicAdd(&ctl->queue, 1);
+            if (q < items) {
+                const int j = q / nb, tile = q % nb, it = it0 + j;
+                const int *stop = &ctl->stop, tm = tile % P.tiles_m, tn = tile / P.tiles_m;
+                // the stop decision of iteration it-2, then the tiles this item reads
+                bool ok = wait_ge(&ctl->fin_it, it - 2, stop) && !ld_agent(stop);
+                ok = ok && wait_ge(&done_it[tile], it - 1, stop);
+                ok = ok && (tm == 0 || wait_ge(&done_it[tile - 1], it - 1, stop));
+                ok = ok && (tm + 1 == P.tiles_m || wait_ge(&done_it[tile + 1], it - 1, stop));
+                ok = ok && (tn == 0 || wait_ge(&done_it[tile - P.tiles_m], it - 1, stop));
+                ok = ok && (tn + 1 == P.tiles_n || wait_ge(&done_it[tile + P.tiles_m], it - 1, stop));
+                if (ok) item = q;
+            }
+            if (GQ_PIPE_FENCES) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sh_item = item;
+        }
+        __syncthreads();
+        const int q = sh_item;
+        if (q < 0) break;  // queue drained or the run stopped
+#if GQ_PIPE_STATS
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#endif
+        const int j = q / nb, tile = q % nb, it = it0 + j;
+        // phase order alternates between consecutive items of a workgroup
+        const bool edge_first = GQ_PHASE_MIX && (((int)blockIdx.x + k) & 1);
+        fix128 *slot = P.partials + (int64_t)(it & 1) * nb * NP;
+        if (edge_first)
+            iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds);
+        else
+            iter_tile<R, VT, ENG, Q, true, false>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            if (GQ_PIPE_FENCES) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st_agent(&done_it[tile], it);
+            atomicAdd(&ctl->arrive2[it & 1], 1);
+#if GQ_PIPE_STATS
+            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+            atomicAdd(&ctl->st_wait, t1 - t0);
+            atomicAdd(&ctl->st_busy, t2 - t1);
+            atomicAdd(&ctl->st_items, 1ull);
+#endif
+        }
+        __syncthreads();
     }
 }
 
@@ -688,6 +952,7 @@ struct gqmap_ctx {
     fix128 *d_partials = nullptr;
     double *d_trace = nullptr;
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
+    int *d_done_it = nullptr;  // pipelined kernel: per-tile completed iteration
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
     int split = 1;      // lanes per node (Q): 1, 4 or 16
@@ -736,7 +1001,11 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     }
     if (c->d_partials) (void)hipFree(c->d_partials);
     c->d_partials = nullptr;
-    GQ_HIP(hipMalloc((void **)&c->d_partials, sizeof(fix128) * (size_t)c->nblocks * (NFIX + c->L) + 64));
+    // two slots: the pipelined kernel has two iterations in flight
+    GQ_HIP(hipMalloc((void **)&c->d_partials, 2 * sizeof(fix128) * (size_t)c->nblocks * (NFIX + c->L) + 64));
+    if (c->d_done_it) (void)hipFree(c->d_done_it);
+    c->d_done_it = nullptr;
+    GQ_HIP(hipMalloc((void **)&c->d_done_it, sizeof(int) * (size_t)c->nblocks));
     return GQMAP_OK;
 }
 
@@ -796,22 +1065,35 @@ FinParams fin_params(const gqmap_ctx *c)
 }
 
 // Resident workgroups per CU for a k_iter instantiation, and CUs per XCD:
-// the tile grouping of k_iter (speed only, never results).
-template <typename R, typename VT, int ENG, int Q>
-void launch_k_iter(gqmap_ctx *c)
+// the tile grouping of k_iter (speed only, never results), and the grid of
+// the pipelined kernel (one workgroup per resident slot).
+template <typename K>
+int2 kernel_shape(K kern)
 {
-    static const int2 shape = [] {
-        int per_cu = 1, dev = 0, cus = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_iter<R, VT, ENG, Q>, BLOCK, 0) != hipSuccess)
-            per_cu = 1;
-        if (hipGetDevice(&dev) == hipSuccess)
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return make_int2(std::max(1, per_cu), std::max(1, cus / 8));
-    }();
+    int per_cu = 1, dev = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK, 0) != hipSuccess) per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return make_int2(std::max(1, per_cu), std::max(8, cus));
+}
+
+template <typename R, typename VT, int ENG, int Q>
+void launch_k_iter(gqmap_ctx *c, int pipe_n)
+{
     IterParams<R, VT> P = iter_params<R, VT>(c);
+    if (pipe_n > 0) {
+        static const int2 shp = kernel_shape(k_iter_pipe<R, VT, ENG, Q>);
+        const int nb = c->nblocks;
+        k_pipe_prep<<<(nb + 255) / 256, 256, 0, c->stream>>>(c->d_ctl, c->d_done_it, nb);
+        // block 0 is the finalizer, the others take items
+        const int grid = (int)std::max<int64_t>(2, std::min<int64_t>((int64_t)shp.x * shp.y, (int64_t)nb * pipe_n + 1));
+        k_iter_pipe<R, VT, ENG, Q><<<grid, BLOCK, 0, c->stream>>>(P, pipe_n, c->d_done_it);
+        return;
+    }
+    static const int2 shape = kernel_shape(k_iter<R, VT, ENG, Q>);
     if (!getenv("GQMAP_NO_CU_GROUP")) {
         P.cu_group = shape.x;
-        P.cu_slots = shape.y;
+        P.cu_slots = std::max(1, shape.y / 8);
         if (const char *g = getenv("GQMAP_CU_GROUP")) P.cu_group = atoi(g);
         if (getenv("GQMAP_CU_GROUP_PRINT")) fprintf(stderr, "k_iter Q=%d cu_group %d cu_slots %d\n", Q, P.cu_group, P.cu_slots);
     }
@@ -819,32 +1101,46 @@ void launch_k_iter(gqmap_ctx *c)
 }
 
 template <typename R, typename VT, int ENG>
-void launch_iter_q(gqmap_ctx *c)
+void launch_iter_q(gqmap_ctx *c, int pipe_n)
 {
     if (c->split == 16)
-        launch_k_iter<R, VT, ENG, 16>(c);
+        launch_k_iter<R, VT, ENG, 16>(c, pipe_n);
     else if (c->split == 4)
-        launch_k_iter<R, VT, ENG, 4>(c);
+        launch_k_iter<R, VT, ENG, 4>(c, pipe_n);
     else
-        launch_k_iter<R, VT, ENG, 1>(c);
+        launch_k_iter<R, VT, ENG, 1>(c, pipe_n);
 }
 
 template <typename R, typename VT>
-void launch_iter_t(gqmap_ctx *c)
+void launch_iter_t(gqmap_ctx *c, int pipe_n)
 {
     switch (c->opt.engine) {
-    case GQMAP_ENGINE_SUPER: launch_iter_q<R, VT, 1>(c); break;
-    case GQMAP_ENGINE_CTF: launch_iter_q<R, VT, 2>(c); break;
-    default: launch_iter_q<R, VT, 0>(c); break;
+    case GQMAP_ENGINE_SUPER: launch_iter_q<R, VT, 1>(c, pipe_n); break;
+    case GQMAP_ENGINE_CTF: launch_iter_q<R, VT, 2>(c, pipe_n); break;
+    default: launch_iter_q<R, VT, 0>(c, pipe_n); break;
     }
 }
 
-void launch_iter(gqmap_ctx *c)
+// pipe_n > 0: one pipelined launch (k_iter_pipe) of pipe_n iterations
+void launch_iter(gqmap_ctx *c, int pipe_n = 0)
 {
-    if (c->fp32) launch_iter_t<float, float>(c);
-    else if (c->vv32) launch_iter_t<double, float>(c);
-    else launch_iter_t<double, double>(c);
+    if (c->fp32) launch_iter_t<float, float>(c, pipe_n);
+    else if (c->vv32) launch_iter_t<double, float>(c, pipe_n);
+    else launch_iter_t<double, double>(c, pipe_n);
 }
+
+// The pipelined kernel applies when nothing an item reads changes between
+// iterations: one Gaussian (no alpha update), constant temperature, a single
+// context (tiles exchange ghosts between launches).  Opt-in (GQMAP_PIPE=1):
+// bit-identical, but on the C2 frame its dynamically dealt tiles lose the L1
+// sharing of co-resident neighbour tiles and run ~1.5x longer each, which
+// costs more than the fill/drain it saves (profiles/r01_kernel_experiments.txt).
+bool use_pipe(const gqmap_ctx *c)
+{
+    const char *e = std::getenv("GQMAP_PIPE");
+    return e && *e == '1' && fused_finalize(c) && c->n_tiles == 1 && c->L == 1 && c->opt.t_decay_every <= 0;
+}
+constexpr int PIPE_CHUNK = 500;  // iterations per pipelined launch
 
 void launch_finalize(gqmap_ctx *c) { k_finalize<<<1, 256, 0, c->stream>>>(fin_params(c)); }
 
@@ -1438,7 +1734,9 @@ gqmap_status gqmap_run(gqmap_ctx *c, int n_iter, int *n_done, double *trace)
         const int chunk = std::min(n_iter - total, TRACE_CAP);
         int left = chunk;
         static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
-        if (left >= GRAPH_CHUNK && !no_graph) {
+        if (use_pipe(c)) {
+            for (; left > 0; left -= std::min(left, PIPE_CHUNK)) launch_iter(c, std::min(left, PIPE_CHUNK));
+        } else if (left >= GRAPH_CHUNK && !no_graph) {
             if ((s = ensure_graph(c)) != GQMAP_OK) return s;
             while (left >= GRAPH_CHUNK) {
                 GQ_HIP(hipGraphLaunch(c->graph, c->stream));
@@ -1477,11 +1775,19 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     std::vector<hipEvent_t> ev((size_t)2 * n_iter + 2);
     for (auto &e : ev) GQ_HIP(hipEventCreate(&e));
     GQ_HIP(hipEventRecord(ev[0], c->stream));
-    for (int i = 0; i < n_iter; ++i) {
+    const bool pipe = use_pipe(c);
+    for (int i = 0; i < n_iter;) {
+        // pipelined: one launch covers up to PIPE_CHUNK iterations, timed as a whole
+        const int n = pipe ? std::min(n_iter - i, PIPE_CHUNK) : 1;
         GQ_HIP(hipEventRecord(ev[2 + 2 * i], c->stream));
-        launch_iter(c);
+        launch_iter(c, pipe ? n : 0);
         GQ_HIP(hipEventRecord(ev[3 + 2 * i], c->stream));
-        if ((s = launch_tail(c)) != GQMAP_OK) return s;
+        if (!pipe && (s = launch_tail(c)) != GQMAP_OK) return s;
+        for (int k = 1; k < n; ++k) {  // empty intervals for the other iterations of the launch
+            GQ_HIP(hipEventRecord(ev[2 + 2 * (i + k)], c->stream));
+            GQ_HIP(hipEventRecord(ev[3 + 2 * (i + k)], c->stream));
+        }
+        i += n;
     }
     GQ_HIP(hipEventRecord(ev[1], c->stream));
     GQ_HIP(hipEventSynchronize(ev[1]));
@@ -1497,6 +1803,9 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     for (auto &e : ev) (void)hipEventDestroy(e);
     Ctl h;
     if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+    if (pipe && GQ_PIPE_STATS)
+        fprintf(stderr, "pipe stats (last launch): items %llu, wait %.3g Mcycles, busy %.3g Mcycles (wait %.1f%%)\n",
+                h.st_items, h.st_wait / 1e6, h.st_busy / 1e6, 100.0 * h.st_wait / (h.st_wait + h.st_busy + 1e-9));
     if (n_done) *n_done = h.it - h0.it;
     if (total_ms) *total_ms = t;
     if (iter_kernel_ms) *iter_kernel_ms = sum;
@@ -1768,7 +2077,8 @@ void gqmap_destroy(gqmap_ctx *c)
     if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);
-    void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace};
+    void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace,
+                    (void *)c->d_done_it};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
