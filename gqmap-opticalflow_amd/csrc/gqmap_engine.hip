@@ -69,6 +69,9 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #ifndef GQ_PIPE_FENCES  // 1: release/acquire fences around tile hand-offs; 0: sc1 stores + sc1 loads
 #define GQ_PIPE_FENCES 0
 #endif
+#ifndef GQ_VV16  // experiment: exact-integer frames stored as _Float16 instead of float (fp64 engine)
+#define GQ_VV16 0
+#endif
 #ifndef GQ_PIPE_STATS  // instrumentation builds only: dependency-wait / busy cycles of the pipelined kernel
 #define GQ_PIPE_STATS 0
 #endif
@@ -90,6 +93,12 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #include "gqmap_math.h"
 
 namespace gq {
+
+#if GQ_VV16
+typedef _Float16 vvs_t;  // compact VV storage of the fp64 engine
+#else
+typedef float vvs_t;
+#endif
 
 constexpr int TILE = 16;
 constexpr int BLOCK = TILE * TILE;
@@ -435,12 +444,13 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
     for (int l = 0; l < P.L; ++l) {
         const R a = R(ctl->alpha[l]);
         const int64_t i = m + (int64_t)M * n + MN * l;
-        R own[NPLANES];
+        // mu_u, mu_v, sigma_u, sigma_v, pn of the node; the four rou planes
+        // are read and updated by their edge jobs
+        R own[5];
 #pragma unroll
-        for (int q = 0; q < NPLANES; ++q) own[q] = valid ? get_state<PIPE>(&src[i + MNL * q]) : R(0);
+        for (int q = 0; q < 5; ++q) own[q] = valid ? get_state<PIPE>(&src[i + MNL * q]) : R(0);
         Grad<R> nd{};
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
-        R drou0 = 0, drou1 = 0, drou2 = 0, drou3 = 0;
         R eE = 0, eda = 0;                                     // sum over the 4 edges
         auto node_phase = [&]() {
         if (inner) {
@@ -482,19 +492,20 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
                 const int64_t r = rm + (int64_t)M * rn + MN * l;
                 const R u1 = own_edge ? (uv ? own[1] : own[0]) : get_state<PIPE>(&src[h + MNL * uv]);
                 const R o1 = own_edge ? (uv ? own[3] : own[2]) : get_state<PIPE>(&src[h + MNL * (2 + uv)]);
-                const R p = own_edge ? (e == 0 ? own[5] : e == 1 ? own[6] : e == 2 ? own[7] : own[8])
-                                     : get_state<PIPE>(&src[h + MNL * (5 + dir + 2 * uv)]);
+                const R p = get_state<PIPE>(&src[h + MNL * (5 + dir + 2 * uv)]);  // rou plane 5+e
                 const R o2 = get_state<PIPE>(&src[r + MNL * (2 + uv)]);
                 const EdgeCoef<R> c = edge_coef(u1, get_state<PIPE>(&src[r + MNL * uv]), o1, o2, p);
                 Sums<R> S = edge_sums(tab, kj, K2, Q, P.epsn, c);
                 if (Q > 1) S = lane_combine<Q>(S);
                 g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p, ENG == 2);
+                // the edge owns its correlation: clamped ascent right here
+                // (gqmap_gpu_mixture.m:46), nothing else reads drou
+                if (own_edge && inner && lead)
+                    put_state<PIPE, R>(&dst[i + MNL * (5 + e)], fmin(fmax(p + g.dp * step, -P.corr), P.corr));
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
                 else         { sum_mu1 = sum_mu1 + g.du1; sum_sg1 = sum_sg1 + g.do1; }
-                if (e == 0) drou0 = g.dp; else if (e == 1) drou1 = g.dp;
-                else if (e == 2) drou2 = g.dp; else drou3 = g.dp;
                 eE = eE + g.E;
                 eda = eda + g.da;
                 // neighbour share: (m+1,n) reads in_up, (m,n+1) reads in_left
@@ -534,10 +545,6 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
             put_state<PIPE, R>(&dst[i + MNL * 2], cl(own[2] + su, P.sig_lo, P.sig_hi));
             put_state<PIPE, R>(&dst[i + MNL * 3], cl(own[3] + sv, P.sig_lo, P.sig_hi));
             put_state<PIPE, R>(&dst[i + MNL * 4], cl(own[4] + nd.dp * step, -P.corr, P.corr));
-            put_state<PIPE, R>(&dst[i + MNL * 5], cl(own[5] + drou0 * step, -P.corr, P.corr));
-            put_state<PIPE, R>(&dst[i + MNL * 6], cl(own[6] + drou1 * step, -P.corr, P.corr));
-            put_state<PIPE, R>(&dst[i + MNL * 7], cl(own[7] + drou2 * step, -P.corr, P.corr));
-            put_state<PIPE, R>(&dst[i + MNL * 8], cl(own[8] + drou3 * step, -P.corr, P.corr));
             // per-node contributions to the global sums (exact fixed point)
             const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
             const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
@@ -1125,7 +1132,7 @@ void launch_iter_t(gqmap_ctx *c, int pipe_n)
 void launch_iter(gqmap_ctx *c, int pipe_n = 0)
 {
     if (c->fp32) launch_iter_t<float, float>(c, pipe_n);
-    else if (c->vv32) launch_iter_t<double, float>(c, pipe_n);
+    else if (c->vv32) launch_iter_t<double, vvs_t>(c, pipe_n);
     else launch_iter_t<double, double>(c, pipe_n);
 }
 
@@ -1386,7 +1393,8 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
         if (c->d_VV) (void)hipFree(c->d_VV);
         if (c->d_I1) (void)hipFree(c->d_I1);
         c->d_VV = c->d_I1 = nullptr;
-        GQ_HIP(hipMalloc(&c->d_VV, (size_t)(Mo + 2) * (No + 2) * (vv32 ? sizeof(float) : sizeof(double))));
+        const size_t vsz = c->fp32 ? sizeof(float) : vv32 ? sizeof(vvs_t) : sizeof(double);
+        GQ_HIP(hipMalloc(&c->d_VV, (size_t)(Mo + 2) * (No + 2) * vsz));
         GQ_HIP(hipMalloc(&c->d_I1, (size_t)Mo * No * c->rsz));
         gqmap_status s = alloc_grid(c);
         if (s != GQMAP_OK) return s;
@@ -1417,7 +1425,8 @@ gqmap_status ctx_set_images_device(gqmap_ctx *c, const double *dI1, const double
     GQ_HIP(pad_vv_device(dI2, Mo, No, d_scratch, c->stream));
     const size_t nvv = (size_t)(Mo + 2) * (No + 2);
     bool vv32 = c->fp32;
-    if (!vv32 && !std::getenv("GQMAP_VV64")) GQ_HIP(f32_exact_device(d_scratch, nvv, d_flag, &vv32, c->stream));
+    if (!vv32 && !std::getenv("GQMAP_VV64") && !GQ_VV16)
+        GQ_HIP(f32_exact_device(d_scratch, nvv, d_flag, &vv32, c->stream));
     gqmap_status s = prepare_images(c, Mo, No, vv32);
     if (s != GQMAP_OK) return s;
     GQ_HIP(convert_device(d_scratch, c->d_VV, nvv, vv32, c->stream));
@@ -1588,12 +1597,16 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
     if (!vv32 && !std::getenv("GQMAP_VV64")) {
         vv32 = true;
         for (double v : VV)
-            if ((double)(float)v != v) { vv32 = false; break; }
+            if ((double)(vvs_t)v != v) { vv32 = false; break; }
     }
     gqmap_status s = prepare_images(c, Mo, No, vv32);
     if (s != GQMAP_OK) return s;
     DeviceGuard dg(c->device);
-    if (vv32) {
+    if (vv32 && !c->fp32) {
+        std::vector<vvs_t> vc(VV.size());
+        for (size_t k = 0; k < VV.size(); ++k) vc[k] = (vvs_t)VV[k];
+        GQ_HIP(hipMemcpy(c->d_VV, vc.data(), vc.size() * sizeof(vvs_t), hipMemcpyHostToDevice));
+    } else if (vv32) {
         std::vector<float> v32(VV.begin(), VV.end());
         GQ_HIP(hipMemcpy(c->d_VV, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice));
     } else if ((s = upload(c, c->d_VV, VV.data(), VV.size())) != GQMAP_OK) {
@@ -1885,8 +1898,8 @@ gqmap_status gqmap_log_p(gqmap_ctx *c, const double *map, double *logp)
             if (c->super_) k_logp<float, float, true><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
             else k_logp<float, float, false><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
         } else if (c->vv32) {
-            if (c->super_) k_logp<double, float, true><<<blocks, 256, 0, c->stream>>>(iter_params<double, float>(c), (const double *)d_map, d_part);
-            else k_logp<double, float, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, float>(c), (const double *)d_map, d_part);
+            if (c->super_) k_logp<double, vvs_t, true><<<blocks, 256, 0, c->stream>>>(iter_params<double, vvs_t>(c), (const double *)d_map, d_part);
+            else k_logp<double, vvs_t, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, vvs_t>(c), (const double *)d_map, d_part);
         } else {
             if (c->super_) k_logp<double, double, true><<<blocks, 256, 0, c->stream>>>(iter_params<double, double>(c), (const double *)d_map, d_part);
             else k_logp<double, double, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, double>(c), (const double *)d_map, d_part);

@@ -168,13 +168,14 @@ GQ_HD R bicubic_cell(VP c, int M2, R so, R to)
     const R a0 = t0 + s1, a1 = t1 * s2, a2 = t2 - s3, a3 = t3 + s0;
     return fma(s3, a3, fma(s2, a2, fma(s1, a1, s0 * a0))) * R(0.25) + (R)(int64_t)(c - (VP)0) * R(1e-30);
 #else
-    const R v0 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    // taps are converted to R exactly (VV storage: double, or float / half when exact)
+    const R v0 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
     c += M2;
-    const R v1 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    const R v1 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
     c += M2;
-    const R v2 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    const R v2 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
     c += M2;
-    const R v3 = fma(c[3], t3, fma(c[2], t2, fma(c[1], t1, c[0] * t0)));
+    const R v3 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
     return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0))) * R(0.25);
 #endif
 }
@@ -262,7 +263,7 @@ GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x
             R v[4];
             GQ_UNROLL_FULL
             for (int di = 0; di < 4; ++di)
-                v[di] = fma(c[di + 3], t3, fma(c[di + 2], t2, fma(c[di + 1], t1, c[di] * t0)));
+                v[di] = fma(R(c[di + 3]), t3, fma(R(c[di + 2]), t2, fma(R(c[di + 1]), t1, R(c[di]) * t0)));
             GQ_UNROLL_FULL
             for (int dj = 0; dj < 4; ++dj) {
                 const int k = a - dj;  // this column is tap k of output column dj
