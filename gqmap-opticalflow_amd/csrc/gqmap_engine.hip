@@ -164,6 +164,7 @@ struct IterParams {
     FinParams fin;
     R epsn, lamd, lams;
     R minu, maxu, minv, maxv, sig_lo, sig_hi, corr, sig_step;
+    R gh_xmax;  // max |Gauss-Hermite node| (node_unclamped)
     double step0, step_decay;
     int guard;
     int64_t MNL;
@@ -319,6 +320,16 @@ __device__ void fin_apply(const FinParams &F, const double *tot)
 // Lane j of a node sums the quadrature points k = j, j+Q, ... and the lanes
 // combine with an xor butterfly (the spec's butterfly()).
 // ---------------------------------------------------------------------------
+// Waves per SIMD the register allocation must allow (MI355X: 136-168 VGPRs
+// -> 3, 176-256 -> 2, more -> 1).  Left to the allocator: forcing 3 waves on
+// the single-scale engine moved arrays to scratch (C2 +24%); bounding the
+// super engine to 2 made its block sum 25% slower than the allocator's own
+// 2-wave (<= 256 VGPR) schedule.  GQ_MIN_WAVES / GQ_SUPER_WAVES: experiments.
+#ifndef GQ_SUPER_WAVES
+#define GQ_SUPER_WAVES 1
+#endif
+constexpr int min_waves(int eng) { return GQ_MIN_WAVES > 1 ? GQ_MIN_WAVES : eng == 1 ? GQ_SUPER_WAVES : 1; }
+
 // Tile index of block b: XCD-aware order.  Blocks b and b+8 share an XCD
 // (round-robin dispatch), so each XCD gets a contiguous band of tiles (L2
 // locality of the VV gathers).  Speed only; results never depend on placement.
@@ -400,7 +411,7 @@ struct TileLds {
 // `parity`): node and edge gradients, neighbour scatter, clamped ascent into
 // the other buffer, and the tile's exact partial sums into part_row[0..NP).
 template <typename R, typename VT, int ENG, int Q, bool PIPE, bool EDGE_FIRST>
-__device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, int it, int parity,
+__device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
                                           fix128 *part_row, TileLds<R, BLOCK / Q> &lds)
 {
     constexpr int TPIX = BLOCK / Q;                   // nodes per tile
@@ -445,23 +456,40 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
         const R a = R(ctl->alpha[l]);
         const int64_t i = m + (int64_t)M * n + MN * l;
         // mu_u, mu_v, sigma_u, sigma_v, pn of the node; the four rou planes
-        // are read and updated by their edge jobs
-        R own[5];
-#pragma unroll
-        for (int q = 0; q < 5; ++q) own[q] = valid ? get_state<PIPE>(&src[i + MNL * q]) : R(0);
+        // are read and updated by their edge jobs.  (Named scalars, not an
+        // array: a select between two array elements by the run-time uv
+        // below would put the array in scratch.)
+        const R mu_u = valid ? get_state<PIPE>(&src[i]) : R(0);
+        const R mu_v = valid ? get_state<PIPE>(&src[i + MNL]) : R(0);
+        const R sg_u = valid ? get_state<PIPE>(&src[i + MNL * 2]) : R(0);
+        const R sg_v = valid ? get_state<PIPE>(&src[i + MNL * 3]) : R(0);
+        const R pn = valid ? get_state<PIPE>(&src[i + MNL * 4]) : R(0);
         Grad<R> nd{};
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R eE = 0, eda = 0;                                     // sum over the 4 edges
-        auto node_phase = [&]() {
+        // Node phase then edge phase, or (EDGE_FIRST) the reverse: the node
+        // phase is gather-heavy, the edge phase pure VALU; mixing the orders
+        // among the workgroups that share a CU overlaps the two.  Both orders
+        // are compile-time straight-line code (the loop below is unrolled; no
+        // lambdas: captured locals ended up in scratch).
+#pragma unroll
+        for (int ph = 0; ph < 2; ++ph) {
+        if ((ph == 0) != EDGE_FIRST) {
+        NodeCoef<R> c{};
+        if (inner) c = node_coef(sg_u, sg_v, pn);
+        // single-scale engine: when no sample of any node of the wave can be
+        // clamped (wave vote), run the quadrature without the clamps
+        const bool fast = ENG == 0 && __all(!inner || node_unclamped(c, mu_u, mu_v, m, n + P.n_off, P.Mo,
+                                                                     P.No, P.gh_xmax));
         if (inner) {
-            const NodeCoef<R> c = node_coef(own[2], own[3], own[4]);
-            Sums<R> S = node_sums<ENG>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
-                                       own[0], own[1], m, n + P.n_off);
+            Sums<R> S = fast ? node_sums<ENG, false>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
+                                                     mu_u, mu_v, m, n + P.n_off)
+                             : node_sums<ENG, true>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
+                                                    mu_u, mu_v, m, n + P.n_off);
             if (Q > 1) S = lane_combine<Q>(S);
-            nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, own[2], own[3], own[4], ENG == 2);
+            nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, sg_u, sg_v, pn, ENG == 2);
         }
-        };
-        auto edge_phase = [&]() {
+        } else {
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
         // edges, then job 4 on the halo lanes: the edges entering the tile from
         // the row above / the column to the left.  One edge body, streamed into
@@ -490,8 +518,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
             if (need) {
                 const int64_t h = hm + (int64_t)M * hn + MN * l;
                 const int64_t r = rm + (int64_t)M * rn + MN * l;
-                const R u1 = own_edge ? (uv ? own[1] : own[0]) : get_state<PIPE>(&src[h + MNL * uv]);
-                const R o1 = own_edge ? (uv ? own[3] : own[2]) : get_state<PIPE>(&src[h + MNL * (2 + uv)]);
+                const R u1 = own_edge ? (uv ? mu_v : mu_u) : get_state<PIPE>(&src[h + MNL * uv]);
+                const R o1 = own_edge ? (uv ? sg_v : sg_u) : get_state<PIPE>(&src[h + MNL * (2 + uv)]);
                 const R p = get_state<PIPE>(&src[h + MNL * (5 + dir + 2 * uv)]);  // rou plane 5+e
                 const R o2 = get_state<PIPE>(&src[r + MNL * (2 + uv)]);
                 const EdgeCoef<R> c = edge_coef(u1, get_state<PIPE>(&src[r + MNL * uv]), o1, o2, p);
@@ -516,17 +544,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
                 else          { in_left[uv][0][hr] = g.du2; in_left[uv][1][hr] = g.do2; }
             }
         }
-        };
-        // Node phase then edge phase, or (EDGE_FIRST) the reverse: the node
-        // phase is gather-heavy, the edge phase pure VALU; mixing the orders
-        // among the workgroups that share a CU overlaps the two.  Each order
-        // is its own straight-line instantiation (registers allocated alone).
-        if (EDGE_FIRST) {
-            edge_phase();
-            node_phase();
-        } else {
-            node_phase();
-            edge_phase();
+        }
         }
         __syncthreads();
         fix128 fda = 0;
@@ -537,14 +555,14 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
             const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][pix]) + in_left[0][1][pix];
             const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
-            put_state<PIPE, R>(&dst[i + MNL * 0], cl(own[0] + gmu_u * step, P.minu, P.maxu));
-            put_state<PIPE, R>(&dst[i + MNL * 1], cl(own[1] + gmu_v * step, P.minv, P.maxv));
+            put_state<PIPE, R>(&dst[i + MNL * 0], cl(mu_u + gmu_u * step, P.minu, P.maxu));
+            put_state<PIPE, R>(&dst[i + MNL * 1], cl(mu_v + gmu_v * step, P.minv, P.maxv));
             // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
             const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
             const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
-            put_state<PIPE, R>(&dst[i + MNL * 2], cl(own[2] + su, P.sig_lo, P.sig_hi));
-            put_state<PIPE, R>(&dst[i + MNL * 3], cl(own[3] + sv, P.sig_lo, P.sig_hi));
-            put_state<PIPE, R>(&dst[i + MNL * 4], cl(own[4] + nd.dp * step, -P.corr, P.corr));
+            put_state<PIPE, R>(&dst[i + MNL * 2], cl(sg_u + su, P.sig_lo, P.sig_hi));
+            put_state<PIPE, R>(&dst[i + MNL * 3], cl(sg_v + sv, P.sig_lo, P.sig_hi));
+            put_state<PIPE, R>(&dst[i + MNL * 4], cl(pn + nd.dp * step, -P.corr, P.corr));
             // per-node contributions to the global sums (exact fixed point)
             const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
             const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
@@ -582,7 +600,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> &P, int tile, 
 }
 
 template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> P)
+__global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT> P)
 {
     Ctl *ctl = P.ctl;
     if (ctl->stop) return;
@@ -590,8 +608,9 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter(IterParams<R, VT> 
     const int b = blockIdx.x;
     const int tile = tile_of_block(b, nb, P.cu_group, P.cu_slots);
     // workgroups that start on one CU are local blocks j, j+S, j+2S of the
-    // XCD (see tile_of_block): alternate the phase order among them
-    const bool edge_first = GQ_PHASE_MIX && (((b >> 3) / P.cu_slots) & 1);
+    // XCD (see tile_of_block): alternate the phase order among them.  Not
+    // for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
+    const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
     const int NP = NFIX + P.L;
     __shared__ TileLds<R, BLOCK / Q> lds;
     if (edge_first)
@@ -726,7 +745,7 @@ __device__ void pipe_finalizer(const FinParams &F0, fix128 *partials, int nb, in
 }
 
 template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter_pipe(IterParams<R, VT> P, int n_iter,
+__global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter_pipe(IterParams<R, VT> P, int n_iter,
                                                                    int *done_it)
 {
     Ctl *ctl = P.ctl;
@@ -774,7 +793,7 @@ __global__ __launch_bounds__(BLOCK, GQ_MIN_WAVES) void k_iter_pipe(IterParams<R,
 #endif
         const int j = q / nb, tile = q % nb, it = it0 + j;
         // phase order alternates between consecutive items of a workgroup
-        const bool edge_first = GQ_PHASE_MIX && (((int)blockIdx.x + k) & 1);
+        const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((int)blockIdx.x + k) & 1);
         fix128 *slot = P.partials + (int64_t)(it & 1) * nb * NP;
         if (edge_first)
             iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds);
@@ -1043,6 +1062,9 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.minu = R(o.minu); P.maxu = R(o.maxu); P.minv = R(o.minv); P.maxv = R(o.maxv);
     P.sig_lo = R(o.sig_lo); P.sig_hi = R(o.sig_hi); P.corr = R(o.corr_tor);
     P.sig_step = R(o.sig_step);
+    double xmax = 0;
+    for (int k = 0; k < c->K2; ++k) xmax = std::max(xmax, std::fabs(c->tab_host[k]));
+    P.gh_xmax = R(xmax);
     P.step0 = o.step0; P.step_decay = o.step_decay;
     P.guard = o.guard_a;
     P.MNL = c->MNL;

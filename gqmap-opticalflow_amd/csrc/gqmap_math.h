@@ -182,32 +182,43 @@ GQ_HD R bicubic_cell(VP c, int M2, R so, R to)
 
 // interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV.
 // fp64: the reference's own position arithmetic (Xq = j + x1, clamp, floor).
-template <typename VP>
+// CLAMP = false: the caller guarantees 1 <= jj + x1 < No and 1 <= ii + x2 < Mo
+// for this sample, where every clamp below is the identity -- same result.
+template <bool CLAMP = true, typename VP>
 GQ_HD double sample(VP VV, int M2, int Mo, int No, int ii, int jj, double x1, double x2)
 {
     // min(max(.,1),N) with MATLAB's NaN-ignoring max/min (IEEE maxNum/minNum)
-    const double Xq = fmin(fmax((double)jj + x1, 1.0), (double)No);
-    const double Yq = fmin(fmax((double)ii + x2, 1.0), (double)Mo);
+    double Xq = (double)jj + x1, Yq = (double)ii + x2;
+    if (CLAMP) {
+        Xq = fmin(fmax(Xq, 1.0), (double)No);
+        Yq = fmin(fmax(Yq, 1.0), (double)Mo);
+    }
     int ix = (int)Xq, iy = (int)Yq;  // Xq >= 1: truncation == floor
-    ix = ix > No - 1 ? No - 1 : ix;
-    iy = iy > Mo - 1 ? Mo - 1 : iy;
+    if (CLAMP) {
+        ix = ix > No - 1 ? No - 1 : ix;
+        iy = iy > Mo - 1 ? Mo - 1 : iy;
+    }
     return bicubic_cell<double>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, Xq - (double)ix,
                                 Yq - (double)iy);
 }
 // fp32: integer + fraction relative to the pixel, so the fractional position
 // keeps full precision at any image size.
-template <typename VP>
+// CLAMP = false: the caller guarantees 1 - jj <= x1 < No - jj and
+// 1 - ii <= x2 < Mo - ii.
+template <bool CLAMP = true, typename VP>
 GQ_HD float sample(VP VV, int M2, int Mo, int No, int ii, int jj, float x1, float x2)
 {
-    const float lox = (float)(1 - jj), hix = (float)(No - jj);
-    const float loy = (float)(1 - ii), hiy = (float)(Mo - ii);
-    x1 = fminf(fmaxf(x1, lox), hix);
-    x2 = fminf(fmaxf(x2, loy), hiy);
+    if (CLAMP) {
+        const float lox = (float)(1 - jj), hix = (float)(No - jj);
+        const float loy = (float)(1 - ii), hiy = (float)(Mo - ii);
+        x1 = fminf(fmaxf(x1, lox), hix);
+        x2 = fminf(fmaxf(x2, loy), hiy);
+    }
     const float fx = floorf(x1), fy = floorf(x2);
     float so = x1 - fx, to = x2 - fy;
     int ix = jj + (int)fx, iy = ii + (int)fy;
-    if (ix > No - 1) { ix = No - 1; so = 1.f; }
-    if (iy > Mo - 1) { iy = Mo - 1; to = 1.f; }
+    if (CLAMP && ix > No - 1) { ix = No - 1; so = 1.f; }
+    if (CLAMP && iy > Mo - 1) { iy = Mo - 1; to = 1.f; }
     return bicubic_cell<float>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, so, to);
 }
 
@@ -477,8 +488,10 @@ GQ_HD NodeCoef<R> node_coef(R o1, R o2, R p)
     c.ay = sq2 * o2 * c.t; c.by = sq2 * o2 * c.s;
     return c;
 }
-// ENG: 0 single-scale mixture, 1 super (4x4 blocks), 2 coarse-to-fine level
-template <int ENG, typename R, typename TP, typename VP, typename IP>
+// ENG: 0 single-scale mixture, 1 super (4x4 blocks), 2 coarse-to-fine level.
+// CLAMP = false (ENG 0): the caller has checked that no sample of this node
+// is clamped (node_unclamped), so the clamps are skipped -- same results.
+template <int ENG, bool CLAMP = true, typename R, typename TP, typename VP, typename IP>
 GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, int Mo, int No,
                         R eps, const NodeCoef<R> &c, R u1, R u2, int m, int n)
 {
@@ -487,7 +500,7 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
         const R I = I1[m + (int64_t)Mo * n];
         auto f_at = [&](R x1, R x2) {
             const R v = ENG == 2 ? sample_ctf(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
-                                 : sample(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
+                                 : sample<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
             const R d = I - v;
             return GQ_SQRT(fma(d, d, eps));
         };
@@ -513,6 +526,19 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
     }
     return S;
 }
+// Conservative test that every quadrature sample of node (m, n) (0-based)
+// lies where sample()'s clamps are the identity: |x1 - u1| <= (|ax|+|bx|) xmax
+// and |x2 - u2| <= (|ay|+|by|) xmax (xmax = max |Gauss-Hermite node|), with a
+// margin far above the rounding of the position arithmetic.
+template <typename R>
+GQ_HD bool node_unclamped(const NodeCoef<R> &c, R u1, R u2, int m, int n, int Mo, int No, R xmax)
+{
+    const R margin = sizeof(R) == 8 ? R(1e-6) : R(1e-2);
+    const R rx = (fabs(c.ax) + fabs(c.bx)) * xmax + margin, ry = (fabs(c.ay) + fabs(c.by)) * xmax + margin;
+    // positions relative to the 1-based pixel (n+1, m+1)
+    return u1 - rx >= R(-n) && u1 + rx < R(No - 1 - n) && u2 - ry >= R(-m) && u2 + ry < R(Mo - 1 - m);
+}
+
 template <typename R>
 GQ_HD Grad<R> node_epi(const Sums<R> &S, const NodeCoef<R> &c, R lamd, bool guard, R T, R a, R o1,
                        R o2, R p, bool raw_energy = false)

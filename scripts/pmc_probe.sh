@@ -14,7 +14,7 @@ for v in $VARS; do
   for P in "$P1" "$P2" "$P3" "$P4"; do
     i=$((i+1))
     GQMAP_LIB=$PWD/gqmap-opticalflow_amd/build/var/libgqmap_$v.so timeout -s KILL 90 rocprofv3 --pmc $P \
-      -d $OUT/${v}_p$i -o run --output-format csv -- python3 scripts/prof_iter.py $ITS $PREC > $OUT/${v}_p$i.log 2>&1
+      -d $OUT/${v}_p$i -o run --output-format csv -- python3 scripts/prof_iter.py $ITS $PREC ${ENGINE:-mixture} > $OUT/${v}_p$i.log 2>&1
     rc=$?; echo "$v p$i rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
 done
