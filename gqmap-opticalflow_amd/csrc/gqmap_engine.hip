@@ -1001,12 +1001,19 @@ struct gqmap_ctx {
 
 namespace {
 
-// Lanes per node: enough lanes for >= 2^17 (8 waves per SIMD... at least
-// 2 per SIMD) on a 256-CU part; the full-resolution 584x388 grid needs none.
-int choose_split(int M, int N, int forced)
+// Lanes per node Q (a node's quadrature split over Q lanes of one wave: more
+// lanes in flight, but lane-varying table indices turn the scalar table loads
+// into vector loads).  Measured per-iteration k_iter times (scripts/
+// level_sweep.py, ctf engine K=11, us for Q = 1 / 4 / 16): 30x40 101/77/41,
+// 60x80 103/78/56, 120x160 108/119/126, 240x320 154/255/388, 480x640
+// 316/715/1287 -> single-pixel engines split only below 2^14 nodes.  The
+// super engine's node (a 4x4 block, 16x the work) keeps splitting up to
+// 2^17 nodes (C4 120x160 x L=3: Q = 1 / 4 / 16 -> 1970 / 780 / 642 us).
+int choose_split(int M, int N, int forced, bool super_)
 {
     if (forced == 1 || forced == 4 || forced == 16) return forced;
     const int64_t nodes = (int64_t)M * N;
+    if (!super_) return nodes >= (1 << 14) ? 1 : 16;
     if (nodes >= (1 << 17)) return 1;
     if (nodes * 4 >= (1 << 17)) return 4;
     return 16;
@@ -1014,7 +1021,7 @@ int choose_split(int M, int N, int forced)
 
 gqmap_status alloc_grid(gqmap_ctx *c)
 {
-    c->split = choose_split(c->M, c->N, c->opt.split);
+    c->split = choose_split(c->M, c->N, c->opt.split, c->super_);
     const int tile = c->split == 1 ? 16 : c->split == 4 ? 8 : 4;
     c->tiles_m = (c->M + tile - 1) / tile;
     c->tiles_n = (c->N + tile - 1) / tile;

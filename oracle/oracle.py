@@ -215,9 +215,11 @@ def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0) -> np.ndarray:
     return out
 
 
-def split_for(M: int, N: int) -> int:
+def split_for(M: int, N: int, super_: bool = False) -> int:
     """The library's default lanes-per-node policy (gqmap_engine.hip choose_split)."""
     nodes = M * N
+    if not super_:
+        return 1 if nodes >= (1 << 14) else 16
     return 1 if nodes >= (1 << 17) else 4 if nodes * 4 >= (1 << 17) else 16
 
 
@@ -236,7 +238,7 @@ def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
     cs = state.cstruct()
     f = lib().emu_run
     f.restype = C.c_int
-    Q = int(opts.get("split", 0)) or (split_for(p.M, p.N) if split is None else split)
+    Q = int(opts.get("split", 0)) or (split_for(p.M, p.N, bool(p.super_)) if split is None else split)
     done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
              _p(trace), nthreads, int(fp32), Q)
     if done < 0:
