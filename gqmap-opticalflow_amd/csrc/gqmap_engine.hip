@@ -599,11 +599,23 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     }
 }
 
+#ifndef GQ_TIMELINE
+#define GQ_TIMELINE 0
+#endif
+#if GQ_TIMELINE
+// debug builds: per-block start / end (s_memrealtime, 100 MHz), HW_ID and
+// XCC_ID of k_iter iteration GQ_TIMELINE (gqmap_debug_timeline)
+__device__ unsigned long long g_timeline[8192 * 4];
+#endif
+
 template <typename R, typename VT, int ENG, int Q>
 __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT> P)
 {
     Ctl *ctl = P.ctl;
     if (ctl->stop) return;
+#if GQ_TIMELINE
+    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int nb = P.tiles_m * P.tiles_n;
     const int b = blockIdx.x;
     const int tile = tile_of_block(b, nb, P.cu_group, P.cu_slots);
@@ -617,6 +629,16 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
         iter_tile<R, VT, ENG, Q, false, true>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds);
     else
         iter_tile<R, VT, ENG, Q, false, false>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds);
+#if GQ_TIMELINE
+    __syncthreads();
+    if (threadIdx.x == 0 && ctl->it == GQ_TIMELINE && b < 8192) {
+        const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();
+        g_timeline[4 * b + 0] = tl0;
+        g_timeline[4 * b + 1] = tl1;
+        g_timeline[4 * b + 2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        g_timeline[4 * b + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+#endif
     if (!P.fused) return;
     const int tid = threadIdx.x;
     // Last workgroup in runs the finalize step: release the partials at
@@ -1490,6 +1512,15 @@ void ctx_adopt_stream(gqmap_ctx *c, hipStream_t s)
 extern "C" {
 
 int gqmap_abi_version(void) { return GQMAP_ABI_VERSION; }
+
+#if GQ_TIMELINE
+// debug builds only (not in include/gqmap.h): copy the k_iter timeline
+int gqmap_debug_timeline(unsigned long long *out, int n)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gq::g_timeline), sizeof(unsigned long long) * 4 * (size_t)n) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
 
 void gqmap_options_default(gqmap_options *o, int engine)
 {
