@@ -160,6 +160,7 @@ struct IterParams {
     // fused finalize: the last workgroup to finish (arrival ticket in Ctl)
     // reduces the partials and runs the k_finalize step in the same launch
     int fused;
+    int lpar;                // 1: a block runs all components of its tile; L: one component per block
     int cu_group, cu_slots;  // co-resident workgroups per CU, CUs per XCD (tile order only)
     FinParams fin;
     R epsn, lamd, lams;
@@ -412,7 +413,7 @@ struct TileLds {
 // the other buffer, and the tile's exact partial sums into part_row[0..NP).
 template <typename R, typename VT, int ENG, int Q, bool PIPE, bool EDGE_FIRST>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
-                                          fix128 *part_row, TileLds<R, BLOCK / Q> &lds)
+                                          fix128 *part_row, TileLds<R, BLOCK / Q> &lds, int l0, int l1)
 {
     constexpr int TPIX = BLOCK / Q;                   // nodes per tile
     constexpr int TM = Q == 1 ? 16 : Q == 4 ? 8 : 4;  // tile side
@@ -452,7 +453,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     constexpr int HALO_LANES = 4 * TM * Q;
     const bool halo_lane = tid < HALO_LANES;
 
-    for (int l = 0; l < P.L; ++l) {
+    for (int l = l0; l < l1; ++l) {
         const R a = R(ctl->alpha[l]);
         const int64_t i = m + (int64_t)M * n + MN * l;
         // mu_u, mu_v, sigma_u, sigma_v, pn of the node; the four rou planes
@@ -594,7 +595,9 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     const int NP = NFIX + P.L;
     if (tid < NP) {  // NP <= 12: all in wave 0
         fix128 v = 0;
-        if (tid < NFIX || P.L > 1) v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
+        const int lq = tid - NFIX;  // dalpha of the components this block ran
+        if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1))
+            v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
         store_fix_agent(&part_row[tid], v);
     }
 }
@@ -618,7 +621,10 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
 #endif
     const int nb = P.tiles_m * P.tiles_n;
     const int b = blockIdx.x;
-    const int tile = tile_of_block(b, nb, P.cu_group, P.cu_slots);
+    // lpar > 1: one block per (tile, component), component-major
+    const int bt = P.lpar > 1 ? b % nb : b;
+    const int l0 = P.lpar > 1 ? b / nb : 0, l1 = P.lpar > 1 ? l0 + 1 : P.L;
+    const int tile = tile_of_block(bt, nb, P.cu_group, P.cu_slots);
     // workgroups that start on one CU are local blocks j, j+S, j+2S of the
     // XCD (see tile_of_block): alternate the phase order among them.  Not
     // for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
@@ -626,9 +632,9 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
     const int NP = NFIX + P.L;
     __shared__ TileLds<R, BLOCK / Q> lds;
     if (edge_first)
-        iter_tile<R, VT, ENG, Q, false, true>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds);
+        iter_tile<R, VT, ENG, Q, false, true>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds, l0, l1);
     else
-        iter_tile<R, VT, ENG, Q, false, false>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds);
+        iter_tile<R, VT, ENG, Q, false, false>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds, l0, l1);
 #if GQ_TIMELINE
     __syncthreads();
     if (threadIdx.x == 0 && ctl->it == GQ_TIMELINE && b < 8192) {
@@ -651,7 +657,7 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
     __shared__ int last;
     if (tid == 0) {
         __builtin_amdgcn_s_waitcnt(0);
-        last = atomicAdd(&ctl->arrive, 1) == nb - 1;
+        last = atomicAdd(&ctl->arrive, 1) == (int)gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
@@ -818,9 +824,9 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter_pipe(IterParams<
         const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((int)blockIdx.x + k) & 1);
         fix128 *slot = P.partials + (int64_t)(it & 1) * nb * NP;
         if (edge_first)
-            iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds);
+            iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds, 0, P.L);
         else
-            iter_tile<R, VT, ENG, Q, true, false>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds);
+            iter_tile<R, VT, ENG, Q, true, false>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds, 0, P.L);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
@@ -1004,6 +1010,7 @@ struct gqmap_ctx {
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
     int split = 1;      // lanes per node (Q): 1, 4 or 16
+    int lpar = 1;       // k_iter blocks per tile (components spread over blocks)
     hipGraphExec_t graph = nullptr;
     bool own_stream = true;
     double tab_host[NTAB * TS];
@@ -1029,25 +1036,39 @@ namespace {
 // level_sweep.py, ctf engine K=11, us for Q = 1 / 4 / 16): 30x40 101/77/41,
 // 60x80 103/78/56, 120x160 108/119/126, 240x320 154/255/388, 480x640
 // 316/715/1287 -> single-pixel engines split only below 2^14 nodes.  The
-// super engine's node (a 4x4 block, 16x the work) keeps splitting up to
-// 2^17 nodes (C4 120x160 x L=3: Q = 1 / 4 / 16 -> 1970 / 780 / 642 us).
-int choose_split(int M, int N, int forced, bool super_)
+// super engine runs its L components as separate blocks (choose_lpar) and
+// counts node-components: C4 (120x160 x L=3 = 57,600) Q = 16 / 4 / 1 ->
+// 616 / 509 / 613-717 us (one block per tile: 680 / 829 / 1687).
+int choose_split(int M, int N, int L, int forced, bool super_)
 {
     if (forced == 1 || forced == 4 || forced == 16) return forced;
     const int64_t nodes = (int64_t)M * N;
     if (!super_) return nodes >= (1 << 14) ? 1 : 16;
-    if (nodes >= (1 << 17)) return 1;
-    if (nodes * 4 >= (1 << 17)) return 4;
+    const int64_t nl = nodes * L;
+    if (nl >= (1 << 17)) return 1;
+    if (nl >= (1 << 14)) return 4;
     return 16;
+}
+
+// Components per k_iter block: the super engine's node grid is 16x smaller
+// than the frame, so its L components run as separate blocks (more
+// workgroups, fewer lanes per node).  Sums are exact fixed point: the split
+// never changes results.  GQMAP_LPAR=1 forces one block per tile.
+int choose_lpar(const gqmap_ctx *c)
+{
+    static const char *e = std::getenv("GQMAP_LPAR");
+    if (e && *e == '1') return 1;
+    return c->super_ && c->L > 1 ? c->L : 1;
 }
 
 gqmap_status alloc_grid(gqmap_ctx *c)
 {
-    c->split = choose_split(c->M, c->N, c->opt.split, c->super_);
+    c->split = choose_split(c->M, c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
     const int tile = c->split == 1 ? 16 : c->split == 4 ? 8 : 4;
     c->tiles_m = (c->M + tile - 1) / tile;
     c->tiles_n = (c->N + tile - 1) / tile;
-    c->nblocks = c->tiles_m * c->tiles_n;
+    c->lpar = choose_lpar(c);
+    c->nblocks = c->tiles_m * c->tiles_n * c->lpar;
     const size_t bytes = (size_t)c->MNL * NPLANES * c->rsz;
     for (int b = 0; b < 2; ++b) {
         if (c->d_st[b]) (void)hipFree(c->d_st[b]);
@@ -1099,6 +1120,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.MNL = c->MNL;
     P.n_off = c->n_off; P.own_lo = c->own_lo; P.own_hi = c->own_hi; P.Ng = c->Ng;
     P.fused = fused_finalize(c);
+    P.lpar = c->lpar;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     return P;

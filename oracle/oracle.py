@@ -215,12 +215,14 @@ def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0) -> np.ndarray:
     return out
 
 
-def split_for(M: int, N: int, super_: bool = False) -> int:
-    """The library's default lanes-per-node policy (gqmap_engine.hip choose_split)."""
+def split_for(M: int, N: int, super_: bool = False, L: int = 1) -> int:
+    """The library's default lanes-per-node policy (gqmap_engine.hip choose_split;
+    the super engine runs its L components as separate blocks: nodes x L)."""
     nodes = M * N
     if not super_:
         return 1 if nodes >= (1 << 14) else 16
-    return 1 if nodes >= (1 << 17) else 4 if nodes * 4 >= (1 << 17) else 16
+    nodes *= L
+    return 1 if nodes >= (1 << 17) else 4 if nodes >= (1 << 14) else 16
 
 
 def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
@@ -238,7 +240,7 @@ def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
     cs = state.cstruct()
     f = lib().emu_run
     f.restype = C.c_int
-    Q = int(opts.get("split", 0)) or (split_for(p.M, p.N, bool(p.super_)) if split is None else split)
+    Q = int(opts.get("split", 0)) or (split_for(p.M, p.N, bool(p.super_), int(p.L)) if split is None else split)
     done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
              _p(trace), nthreads, int(fp32), Q)
     if done < 0:
