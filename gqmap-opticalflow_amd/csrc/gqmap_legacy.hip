@@ -49,6 +49,8 @@ __device__ __forceinline__ size_t i5(int M, int N, int m, int n, int j, int q, i
     return m + (size_t)M * (n + (size_t)N * (j + 2 * (q + 5 * (size_t)l)));
 }
 
+// GAMA1 / VAR1: gama == 1 / var == 1, where x / 1 == x exactly (no division)
+template <bool GAMA1, bool VAR1>
 __global__ void k_legacy_grad(LgParams P)
 {
     if (P.ctl[1]) return;
@@ -62,7 +64,7 @@ __global__ void k_legacy_grad(LgParams P)
         double du = 0, dsum = 0;
         for (int k = 0; k < K; ++k) {
             const double x = sq2 * o * P.X[k] + u;
-            const double dval = P.W[k] * (f - x) / P.var;
+            const double dval = VAR1 ? P.W[k] * (f - x) : P.W[k] * (f - x) / P.var;
             du += dval;
             dsum += dval * P.X[k];
         }
@@ -88,7 +90,7 @@ __global__ void k_legacy_grad(LgParams P)
                     const double x1 = sq2 * o1 * ZI + u1, x2 = sq2 * o2 * ZJ + u2;
                     double diff = x2 - x1;
                     if (fabs(diff) > P.dta) diff = 0;  // (:44)
-                    const double df1 = ww * diff / P.gama, df2 = -df1;
+                    const double df1 = GAMA1 ? ww * diff : ww * diff / P.gama, df2 = -df1;
                     c1 += df1;
                     c2 += df2;
                     co1 += df1 * ZI;
@@ -106,9 +108,32 @@ __global__ void k_legacy_grad(LgParams P)
     }
 }
 
-__device__ __forceinline__ void amax(unsigned long long *slot, double v)
+// |v| as its bit pattern: for |v| >= 0 (and NaN above +inf) the unsigned
+// order of the bits is the order of the values, so max is exact in any order
+__device__ __forceinline__ unsigned long long abits(double v)
 {
-    atomicMax(slot, (unsigned long long)__double_as_longlong(fabs(v)));  // |v| >= 0: bits order as values
+    return (unsigned long long)__double_as_longlong(fabs(v));
+}
+
+// Block maximum of three bit patterns, then one atomicMax per slot and block
+// (one atomic per thread on three addresses serialised in L2: 240 us/launch).
+__device__ void block_amax3(unsigned long long *slot, unsigned long long a, unsigned long long b,
+                            unsigned long long c)
+{
+    __shared__ unsigned long long red[3][4];
+    for (int o = 32; o > 0; o >>= 1) {
+        a = max(a, __shfl_xor(a, o));
+        b = max(b, __shfl_xor(b, o));
+        c = max(c, __shfl_xor(c, o));
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) { red[0][wave] = a; red[1][wave] = b; red[2][wave] = c; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int q = threadIdx.x;
+        const unsigned long long v = max(max(red[q][0], red[q][1]), max(red[q][2], red[q][3]));
+        if (v) atomicMax(slot + q, v);
+    }
 }
 
 __global__ void k_legacy_update(LgParams P)
@@ -116,9 +141,13 @@ __global__ void k_legacy_update(LgParams P)
     if (P.ctl[1]) return;
     const int M = P.M, N = P.N;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)M * N * 2) return;
-    const int m = (int)(t % M), n = (int)((t / M) % N), l = (int)(t / ((int64_t)M * N));
     const int it = P.ctl[0];
+    unsigned long long *slot = P.maxbits + 3 * (size_t)(it - 1);
+    if (t >= (int64_t)M * N * 2) {  // still takes part in the block maximum
+        block_amax3(slot, 0, 0, 0);
+        return;
+    }
+    const int m = (int)(t % M), n = (int)((t / M) % N), l = (int)(t / ((int64_t)M * N));
     const double *de = P.dedge;
     // (:58-59) dmu = dnode + sum_j dedge(:,:,j,1) + (dedge(m+1,n,1,2) + dedge(m,n+1,2,2))
     double a = P.dnode[i4(M, N, m, n, 0, l)] + (de[i5(M, N, m, n, 0, 0, l)] + de[i5(M, N, m, n, 1, 0, l)]);
@@ -140,10 +169,15 @@ __global__ void k_legacy_update(LgParams P)
         const size_t r = i4(M, N, m, n, j, l);
         P.rou[r] = fmax(fmin(P.rou[r] + d * step, P.corr), -P.corr);
     }
-    unsigned long long *slot = P.maxbits + 3 * (size_t)(it - 1);
-    amax(slot + 0, a);
-    amax(slot + 1, b);
-    amax(slot + 2, mp);
+    block_amax3(slot, abits(a), abits(b), abits(mp));
+}
+
+// sigma = rand(M,N,2) + 2 (:10) from the library RNG stream 3: the host
+// formula, evaluated on the device
+__global__ void k_legacy_sigma0(double *sigma, int64_t n, uint64_t base)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sigma[i] = u01(base, (uint64_t)i) + 2;
 }
 
 __global__ void k_legacy_ctl(LgParams P)
@@ -208,14 +242,8 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
         return GQMAP_ERR_INVALID_ARG;
     }
     const size_t MN = (size_t)M * N;
-    // mu = flow (:9); sigma = rand(M,N,2) + 2 (:10, library RNG stream 3) unless given; rou = 0 (:11)
-    std::vector<double> sg0(2 * MN);
-    if (sigma0) {
-        std::memcpy(sg0.data(), sigma0, sizeof(double) * 2 * MN);
-    } else {
-        gqmap_rand_uniform(seed, 3, 0, 2 * MN, sg0.data());
-        for (double &v : sg0) v = v + 2;
-    }
+    // mu = flow (:9); sigma = rand(M,N,2) + 2 (:10, library RNG stream 3,
+    // drawn on the device) unless given; rou = 0 (:11)
     struct Buf {
         void *p = nullptr;
         ~Buf() { if (p) (void)hipFree(p); }
@@ -230,8 +258,11 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     GQ_HIP(hipMalloc(&bctl.p, sizeof(int) * 4));
     GQ_HIP(hipMalloc(&btr.p, sizeof(double) * 3 * (size_t)o->its));
     GQ_HIP(hipMemcpy(bflow.p, flow, sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
-    GQ_HIP(hipMemcpy(bmu.p, flow, sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
-    GQ_HIP(hipMemcpy(bsg.p, sg0.data(), sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
+    GQ_HIP(hipMemcpy(bmu.p, bflow.p, sizeof(double) * 2 * MN, hipMemcpyDeviceToDevice));
+    if (sigma0)
+        GQ_HIP(hipMemcpy(bsg.p, sigma0, sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
+    else
+        k_legacy_sigma0<<<(int)((2 * MN + 255) / 256), 256>>>((double *)bsg.p, (int64_t)(2 * MN), stream_base(seed, 3));
     GQ_HIP(hipMemset(brou.p, 0, sizeof(double) * 4 * MN));
     GQ_HIP(hipMemset(bdn.p, 0, sizeof(double) * 4 * MN));   // dnode = zeros (:14): last row/col stay 0
     GQ_HIP(hipMemset(bde.p, 0, sizeof(double) * 20 * MN));  // dedge = zeros (:15)
@@ -242,8 +273,10 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     P.dnode = (double *)bdn.p; P.dedge = (double *)bde.p; P.maxbits = (unsigned long long *)bmax.p;
     P.ctl = (int *)bctl.p; P.trace = (double *)btr.p;
     const int g1 = (int)(((int64_t)(M - 1) * (N - 1) + 255) / 256), g2 = (int)((2 * (int64_t)MN + 255) / 256);
+    auto grad = P.gama == 1.0 ? (P.var == 1.0 ? k_legacy_grad<true, true> : k_legacy_grad<true, false>)
+                              : (P.var == 1.0 ? k_legacy_grad<false, true> : k_legacy_grad<false, false>);
     for (int it = 0; it < o->its; ++it) {
-        k_legacy_grad<<<g1, 256>>>(P);
+        grad<<<g1, 256>>>(P);
         k_legacy_update<<<g2, 256>>>(P);
         k_legacy_ctl<<<1, 1>>>(P);
     }
