@@ -75,6 +75,9 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #ifndef GQ_PIPE_STATS  // instrumentation builds only: dependency-wait / busy cycles of the pipelined kernel
 #define GQ_PIPE_STATS 0
 #endif
+#ifndef GQ_TAB_LDS
+#define GQ_TAB_LDS 1
+#endif
 #ifndef GQ_PHASE_MIX
 #define GQ_PHASE_MIX 1
 #endif
@@ -406,6 +409,9 @@ struct TileLds {
     R in_up[2][2][TPIX];
     R in_left[2][2][TPIX];
     fix128 red[GQMAP_LMAX + NFIX][4];
+    // Q > 1: the quadrature table, so lane-varying table reads are LDS reads
+    // (with Q lanes per node the index k differs across a wave's lanes)
+    R tab[TPIX < BLOCK && GQ_TAB_LDS ? NTAB * TS : 1];
 };
 
 // One tile of one iteration (absolute iteration `it`, reading state buffer
@@ -439,8 +445,20 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     };
     const bool inner = valid && interior(m, n);
     const bool lead = kj == 0;  // the lane that owns the node's outputs
-    const ctab_t<R> tab = as_const(P.tab);
     const int K2 = P.K2;
+    constexpr bool TAB_LDS = Q > 1 && GQ_TAB_LDS;
+    using tab_t = std::conditional_t<TAB_LDS, const R *, ctab_t<R>>;
+    tab_t tab;
+    if constexpr (TAB_LDS) {
+        for (int e = threadIdx.x; e < NTAB * K2; e += BLOCK) {
+            const int r = e / K2, k = e - r * K2;
+            lds.tab[r * TS + k] = P.tab[r * TS + k];
+        }
+        __syncthreads();
+        tab = lds.tab;
+    } else {
+        tab = as_const(P.tab);
+    }
 
     auto &in_up = lds.in_up;
     auto &in_left = lds.in_left;
@@ -1031,19 +1049,20 @@ struct gqmap_ctx {
 namespace {
 
 // Lanes per node Q (a node's quadrature split over Q lanes of one wave: more
-// lanes in flight, but lane-varying table indices turn the scalar table loads
-// into vector loads).  Measured per-iteration k_iter times (scripts/
-// level_sweep.py, ctf engine K=11, us for Q = 1 / 4 / 16): 30x40 101/77/41,
-// 60x80 103/78/56, 120x160 108/119/126, 240x320 154/255/388, 480x640
-// 316/715/1287 -> single-pixel engines split only below 2^14 nodes.  The
-// super engine runs its L components as separate blocks (choose_lpar) and
-// counts node-components: C4 (120x160 x L=3 = 57,600) Q = 16 / 4 / 1 ->
-// 616 / 509 / 613-717 us (one block per tile: 680 / 829 / 1687).
+// lanes in flight; the lane-varying table index is served from an LDS copy of
+// the quadrature table).  Measured per-iteration k_iter times (scripts/
+// level_sweep.py, ctf engine K=11, us for Q = 1 / 4 / 16): 30x40 102/48/35,
+// 60x80 103/48/45, 120x160 108/72/99, 240x320 158/161/329, 480x640
+// 309/467/1170 -> single-pixel engines: Q = 16 below 2^13 nodes, 4 below
+// 2^16, else 1.  The super engine runs its L components as separate blocks
+// (choose_lpar) and counts node-components: C4 (120x160 x L=3 = 57,600)
+// Q = 16 / 4 / 1 -> 616 / 509 / 613-717 us with global table reads (one block
+// per tile: 680 / 829 / 1687); Q = 4 with the LDS table 376 us.
 int choose_split(int M, int N, int L, int forced, bool super_)
 {
     if (forced == 1 || forced == 4 || forced == 16) return forced;
     const int64_t nodes = (int64_t)M * N;
-    if (!super_) return nodes >= (1 << 14) ? 1 : 16;
+    if (!super_) return nodes >= (1 << 16) ? 1 : nodes >= (1 << 13) ? 4 : 16;
     const int64_t nl = nodes * L;
     if (nl >= (1 << 17)) return 1;
     if (nl >= (1 << 14)) return 4;
@@ -1063,7 +1082,9 @@ int choose_lpar(const gqmap_ctx *c)
 
 gqmap_status alloc_grid(gqmap_ctx *c)
 {
-    c->split = choose_split(c->M, c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
+    // from the whole grid (Ng columns), so every column-strip tile sums its
+    // quadrature in the same order as the untiled solve
+    c->split = choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
     const int tile = c->split == 1 ? 16 : c->split == 4 ? 8 : 4;
     c->tiles_m = (c->M + tile - 1) / tile;
     c->tiles_n = (c->N + tile - 1) / tile;
