@@ -92,7 +92,8 @@ def imwrite(img: np.ndarray, path: str) -> None:
 
 
 def middlebury_names():
-    return sorted(d for d in os.listdir(DATA_DIR) if os.path.isdir(os.path.join(DATA_DIR, d)))
+    return sorted(d for d in os.listdir(DATA_DIR)
+                  if d != "preprocessed" and os.path.isdir(os.path.join(DATA_DIR, d)))
 
 
 def load_pair(name: str, root: str = DATA_DIR):
@@ -102,3 +103,18 @@ def load_pair(name: str, root: str = DATA_DIR):
     I2 = rgb2gray(imread(os.path.join(d, "frame11.png"))).astype(np.float64)
     gt = read_flow_file(os.path.join(d, "flow10.flo"))
     return np.asfortranarray(I1), np.asfortranarray(I2), gt
+
+
+def load_preprocessed(name: str, root: str = DATA_DIR):
+    """optical_flowSuper.m:7-14 with preprocessed=true: the structure-texture
+    frames the reference loads from middlebury/preprocessed/<name>.mat
+    (img1, img2; fp64, not integer-valued), plus the GT flow of the pair.
+    Stored here as .npz (scripts/make_preprocessed_fixture.py)."""
+    path = os.path.join(root, "preprocessed", name + ".npz")
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"no preprocessed frames for {name!r} ({path})")
+    with np.load(path) as d:
+        I1, I2 = d["img1"], d["img2"]
+    pair = name if os.path.isdir(os.path.join(root, name)) else name.lower()
+    gt = read_flow_file(os.path.join(root, pair, "flow10.flo"))
+    return np.asfortranarray(I1, dtype=np.float64), np.asfortranarray(I2, dtype=np.float64), gt

@@ -420,3 +420,18 @@ def test_invalid_arguments_raise():
     with Engine(d["opts"], d["I1"], d["I2"]) as eng:
         with pytest.raises(_lib.GqmapError):
             eng.run(1)  # no state yet
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_super_bit_exact_on_preprocessed_frames(precision):
+    # optical_flowSuper.m preprocessed=true: non-integer structure-texture frames
+    # (fp64 VV store), 20 iterations, bit-exact vs the CPU model
+    from gqmap_opticalflow_amd import Engine
+    from tests.test_preprocessed import _case
+    I1, I2, o, st = _case()
+    e_done, e_tr, e_T, ost = _emulate(o, I1, I2, st, 20, precision, None)
+    with Engine(o, I1, I2, "super", precision) as eng:
+        eng.set_state(st)
+        done, tr = eng.run(20)
+        g = eng.get_state()
+    _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
