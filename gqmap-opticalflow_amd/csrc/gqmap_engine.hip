@@ -75,6 +75,9 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #ifndef GQ_PIPE_STATS  // instrumentation builds only: dependency-wait / busy cycles of the pipelined kernel
 #define GQ_PIPE_STATS 0
 #endif
+#ifndef GQ_FIN_GROUP
+#define GQ_FIN_GROUP 1  // finalize: the NFIX fixed sums loaded together (fp32 C2 -2 us)
+#endif
 #ifndef GQ_TAB_LDS
 #define GQ_TAB_LDS 1
 #endif
@@ -241,12 +244,29 @@ __device__ __forceinline__ fix128 load_fix_agent(const fix128 *p)
 // tot[] (LDS), all 256 threads of one workgroup.
 __device__ void fin_reduce(const FinParams &F, double *tot, fix128 *sh)
 {
-    // one quantity at a time (few live registers: this code shares the
-    // k_iter register budget when the finalize is fused)
+    // the NFIX fixed sums together, the dalpha sums one at a time (few live
+    // registers: this code shares the k_iter register budget when fused)
     const int NP = NFIX + F.L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rows = F.nranks > 0 ? F.nranks : F.nblocks;
+#if GQ_FIN_GROUP
+    {   // the NFIX fixed quantities together: a row's loads in flight at once
+        fix128 v[NFIX] = {};
+        for (int r = tid; r < rows; r += 256) {
+#pragma unroll
+            for (int q = 0; q < NFIX; ++q)
+                v[q] += F.nranks > 0 ? F.gathered[(int64_t)r * NP + q] : load_fix_agent(F.partials + (int64_t)r * NP + q);
+        }
+#pragma unroll
+        for (int q = 0; q < NFIX; ++q) {
+            const fix128 w = wave_sum_fix(v[q]);
+            if (lane == 0) sh[q * 4 + wave] = w;
+        }
+    }
+    for (int q = NFIX; q < NP; ++q) {
+#else
     for (int q = 0; q < NP; ++q) {
+#endif
         fix128 v = 0;
         for (int r = tid; r < rows; r += 256)
             v += F.nranks > 0 ? F.gathered[(int64_t)r * NP + q] : load_fix_agent(F.partials + (int64_t)r * NP + q);
