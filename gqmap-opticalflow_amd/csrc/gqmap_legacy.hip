@@ -244,19 +244,39 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     const size_t MN = (size_t)M * N;
     // mu = flow (:9); sigma = rand(M,N,2) + 2 (:10, library RNG stream 3,
     // drawn on the device) unless given; rou = 0 (:11)
-    struct Buf {
+    // One device arena per host thread and device, kept across calls: the
+    // nine buffers (~300 B per pixel) are carved from it, so a repeated call
+    // pays no hipMalloc/hipFree (they dominated a 50-iteration call's wall clock).
+    struct Buf { void *p = nullptr; };
+    Buf bflow, bmu, bsg, brou, bdn, bde, bmax, bctl, btr;
+    struct Arena {
         void *p = nullptr;
-        ~Buf() { if (p) (void)hipFree(p); }
-    } bflow, bmu, bsg, brou, bdn, bde, bmax, bctl, btr;
-    GQ_HIP(hipMalloc(&bflow.p, sizeof(double) * 2 * MN));
-    GQ_HIP(hipMalloc(&bmu.p, sizeof(double) * 2 * MN));
-    GQ_HIP(hipMalloc(&bsg.p, sizeof(double) * 2 * MN));
-    GQ_HIP(hipMalloc(&brou.p, sizeof(double) * 4 * MN));
-    GQ_HIP(hipMalloc(&bdn.p, sizeof(double) * 4 * MN));
-    GQ_HIP(hipMalloc(&bde.p, sizeof(double) * 20 * MN));
-    GQ_HIP(hipMalloc(&bmax.p, sizeof(unsigned long long) * 3 * (size_t)o->its));
-    GQ_HIP(hipMalloc(&bctl.p, sizeof(int) * 4));
-    GQ_HIP(hipMalloc(&btr.p, sizeof(double) * 3 * (size_t)o->its));
+        size_t cap = 0;
+        ~Arena() { if (p) (void)hipFree(p); }
+    };
+    constexpr int kMaxDev = 64;
+    thread_local Arena arenas[kMaxDev];
+    GQ_CHECK(device < kMaxDev, GQMAP_ERR_INVALID_ARG, "device %d >= %d", device, kMaxDev);
+    const size_t sizes[9] = {sizeof(double) * 2 * MN, sizeof(double) * 2 * MN, sizeof(double) * 2 * MN,
+                             sizeof(double) * 4 * MN, sizeof(double) * 4 * MN, sizeof(double) * 20 * MN,
+                             sizeof(unsigned long long) * 3 * (size_t)o->its, sizeof(int) * 4,
+                             sizeof(double) * 3 * (size_t)o->its};
+    Buf *bufs[9] = {&bflow, &bmu, &bsg, &brou, &bdn, &bde, &bmax, &bctl, &btr};
+    size_t need = 0;
+    for (size_t sz : sizes) need += (sz + 255) & ~(size_t)255;
+    Arena &A = arenas[device];
+    if (A.cap < need) {
+        if (A.p) GQ_HIP(hipFree(A.p));
+        A.p = nullptr; A.cap = 0;
+        const size_t cap = need + need / 8;  // headroom: a longer run reuses it
+        GQ_HIP(hipMalloc(&A.p, cap));
+        A.cap = cap;
+    }
+    size_t off = 0;
+    for (int i = 0; i < 9; ++i) {
+        bufs[i]->p = (char *)A.p + off;
+        off += (sizes[i] + 255) & ~(size_t)255;
+    }
     GQ_HIP(hipMemcpy(bflow.p, flow, sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
     GQ_HIP(hipMemcpy(bmu.p, bflow.p, sizeof(double) * 2 * MN, hipMemcpyDeviceToDevice));
     if (sigma0)
