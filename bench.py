@@ -19,8 +19,12 @@ named in `config`):
     --config c3   Grove3 480x640, 5-level coarse-to-fine pyramid (gqmap_ctf
                   levels + device imresize/warp/fillmissing), steps = its/level
     --config c4   Urban3 480x640, gqmap_gpuSuper_mix_entropy L=3 K=11, 1000 its
-    --config c5   RubberWhale upsampled 4x (1552x2336), column-strip tiles over
-                  the ranks with RCCL ghost-column exchange (strong scaling)
+    --config c5   the eight GT pairs of legacy/optical_flow_temp.m:3 upsampled
+                  4x (33.1 Mpx in all), each pair split into column-strip
+                  tiles over the ranks with RCCL ghost-column exchange, pairs
+                  in turn (strong scaling)
+    --config c2 --tiled   the RubberWhale pair itself split over the ranks
+                  (strong scaling of the headline pair)
     --config c1   Dimetrodon 388x584 legacy/gqmap_cpu.m flow denoising, 50 its
                   (device drop-in; timed call includes its host<->device copies)
 Rank 0 prints one JSON line.
@@ -43,6 +47,8 @@ PEAK_TFLOPS = {"fp64": 78.6, "fp32": 157.3}   # MI355X vector (non-MFMA) peaks, 
 PEAK_HBM_GBPS = 8000.0
 PAIRS = ("rubberwhale", "Dimetrodon", "Hydrangea")      # the 584x388 Middlebury pairs
 PAIRS_480 = ("Grove3", "Urban3", "Urban2", "Grove2")     # the 640x480 pairs
+# the eight GT pairs of legacy/optical_flow_temp.m:3 (config C5), as flowio.C5_PAIRS
+C5_PAIRS = ("Urban3", "Grove3", "Urban2", "Venus", "Dimetrodon", "rubberwhale", "Grove2", "Hydrangea")
 DEFAULT_STEPS = {"c1": 50, "c2": 500, "c3": 500, "c4": 1000, "c5": 100}
 
 
@@ -74,27 +80,76 @@ def setup_problem(name: str, L: int, K: int):
     return gt_options(name, L, K)
 
 
-def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 12.0):
-    """The oracle (literal C fp64 restatement, OpenMP) on this host's cores,
-    on a bounded sample of the same workload."""
-    from gqmap_opticalflow_amd import initial_state
-    from oracle import oracle
-    threads = min(16, os.cpu_count() or 1)
-    Mo, No = I1.shape
-    M, N = (Mo // 4, No // 4) if engine == "super" else (Mo, No)
-    o = dict(opts, engine=engine)
-    st0 = initial_state(o, M, N, seed=0, engine=engine)
-    st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
+def host_cpus():
+    """What the CPU baseline runs on: nproc, the threads this process may use
+    (affinity, capped by OMP_NUM_THREADS -- the GPU box grants each GPU a
+    share of its cores and sets OMP_NUM_THREADS to it), physical cores."""
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = nproc
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
+    phys = set()
+    try:
+        pid = cid = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                cid = line.split(":")[1].strip()
+            elif not line.strip():
+                if cid is not None:
+                    phys.add((pid, cid))
+                pid = cid = None
+    except OSError:
+        pass
+    return {"nproc": nproc, "affinity": avail, "threads": threads, "physical_cores": len(phys) or None}
+
+
+def _timed_leg(run_n, budget_s):
+    """Time run_n(n) on a bounded sample: one probe iteration sizes n to
+    about budget_s seconds.  Returns (iterations, seconds)."""
     t0 = time.perf_counter()
-    oracle.run(o, I1, I2, st, 1, 1, nthreads=threads)
+    run_n(1)
     t1 = time.perf_counter() - t0
     n = max(1, min(200, int(budget_s / max(t1, 1e-3))))
     t0 = time.perf_counter()
-    done, _, _ = oracle.run(o, I1, I2, st, 2, n, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": Mo * No * done / dt / 1e9, "unit": "Gpixel-iter/s", "cores": threads, "kind": "port",
+    done = run_n(n)
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 8.0):
+    """The oracle (literal C fp64 restatement of the engine loop, OpenMP over
+    rows) on this host's cores -- every core this process may use, then one
+    thread -- on a bounded sample of the same workload."""
+    from gqmap_opticalflow_amd import initial_state
+    from oracle import oracle
+    hc = host_cpus()
+    Mo, No = I1.shape
+    M, N = (Mo // 4, No // 4) if engine == "super" else (Mo, No)
+    o = dict(opts, engine=engine)
+    legs = {}
+    for threads in (hc["threads"], 1):
+        st0 = initial_state(o, M, N, seed=0, engine=engine)
+        st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
+        it = [1]
+
+        def run_n(n, st=st, threads=threads):
+            done, _, _ = oracle.run(o, I1, I2, st, it[0], n, nthreads=threads)
+            it[0] += done
+            return done
+        legs[threads] = _timed_leg(run_n, budget_s)
+    (n_all, t_all), (n_one, t_one) = legs[hc["threads"]], legs[1]
+    return {"value": Mo * No * n_all / t_all / 1e9, "unit": "Gpixel-iter/s", "cores": hc["threads"],
+            "kind": "port", "value_1thread": Mo * No * n_one / t_one / 1e9,
+            "nproc": hc["nproc"], "affinity_cpus": hc["affinity"], "physical_cores": hc["physical_cores"],
             "sample": f"oracle/gqmap_oracle.c fp64 ({engine}), {label} {No}x{Mo}, L={opts['L']} K={opts['K']}, "
-                      f"iterations 2..{done + 1} from the seeded init, {threads} OpenMP threads, {dt:.1f}s"}
+                      f"seeded init: {n_all} iterations on {hc['threads']} OpenMP threads in {t_all:.1f}s "
+                      f"(the process's CPU share: nproc {hc['nproc']}, affinity {hc['affinity']}, "
+                      f"OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS', 'unset')}), then {n_one} iterations "
+                      f"on 1 thread in {t_one:.1f}s"}
 
 
 def traffic_per_launch(precision: str, config: str):
@@ -200,68 +255,96 @@ def run_c1(args, rank, world, local, barrier):
                          f"call's host<->device copies; aepe = mean |mu - flow|")
 
 
-def cpu_baseline_c1(flow, opts):
-    """The C restatement of legacy/gqmap_cpu.m (single thread, as the MATLAB
-    parfor would run on one worker), bounded sample."""
+def cpu_baseline_c1(flow, opts, budget_s: float = 8.0):
+    """The C restatement of legacy/gqmap_cpu.m, OpenMP over rows as the
+    reference's parfor (legacy/gqmap_cpu.m:17) -- all of this process's
+    cores, then one thread -- on a bounded sample."""
     from gqmap_opticalflow_amd import gauss_hermite
     from oracle import oracle
+    hc = host_cpus()
     M, N, _ = flow.shape
     X, W = gauss_hermite(9)
     sg0 = np.asfortranarray(np.full((M, N, 2), 2.5))
-    t0 = time.perf_counter()
-    oracle.cpu_run(dict(opts, its=1), flow, sg0, X, W)
-    t1 = time.perf_counter() - t0
-    n = max(1, min(opts["its"], int(10.0 / max(t1, 1e-3))))
-    t0 = time.perf_counter()
-    _, _, _, tr = oracle.cpu_run(dict(opts, its=n), flow, sg0, X, W)
-    dt = time.perf_counter() - t0
-    return {"value": M * N * tr.shape[0] / dt / 1e9, "unit": "Gpixel-iter/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/gqmap_legacy_oracle.c fp64, {N}x{M}, K=9, {tr.shape[0]} iterations, 1 thread, {dt:.1f}s"}
+    legs = {}
+    for threads in (hc["threads"], 1):
+        def run_n(n, threads=threads):
+            return oracle.cpu_run(dict(opts, its=n, min_its=10 ** 9), flow, sg0, X, W, nthreads=threads)[3].shape[0]
+        legs[threads] = _timed_leg(run_n, budget_s)
+    (n_all, t_all), (n_one, t_one) = legs[hc["threads"]], legs[1]
+    return {"value": M * N * n_all / t_all / 1e9, "unit": "Gpixel-iter/s", "cores": hc["threads"], "kind": "port",
+            "value_1thread": M * N * n_one / t_one / 1e9, "nproc": hc["nproc"],
+            "affinity_cpus": hc["affinity"], "physical_cores": hc["physical_cores"],
+            "sample": f"oracle/gqmap_legacy_oracle.c fp64, {N}x{M}, K=9: {n_all} iterations on {hc['threads']} "
+                      f"OpenMP threads (rows, as the reference parfor) in {t_all:.1f}s, {n_one} on 1 thread "
+                      f"in {t_one:.1f}s"}
 
 
-def run_c5(args, rank, world, local, barrier, dist):
-    """RubberWhale bicubic-upsampled 4x (frames with the device imresize, GT
-    x4 in size and value), column-strip tiles over the ranks."""
-    from gqmap_opticalflow_amd import Engine, aepe, comm_unique_id, flow_to_color, flowio, imresize
-    I1s, I2s, gt = flowio.load_pair("rubberwhale")
-    # imresize of the uint8 frames as the drivers do (imresize(imread(..),scale),
-    # optical_flowSuper.m:8-9): round half away from zero and saturate to uint8
-    u8 = lambda a: np.asfortranarray(np.clip(np.sign(a) * np.floor(np.abs(a) + 0.5), 0, 255))
-    I1, I2 = u8(imresize(I1s, 4.0, device=local)), u8(imresize(I2s, 4.0, device=local))
-    # GT x4 in value (unknown entries stay > 1e9) and in size (nearest)
-    gt4 = np.asfortranarray(np.repeat(np.repeat(gt * 4.0, 4, axis=0), 4, axis=1))
-    _, flo, (minu, maxu, minv, maxv), unk = flow_to_color(gt4, device=local)
-    opts = dict(its=args.steps, K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdas=5.0, lambdad=1.0,
-                minu=minu, maxu=maxu, minv=minv, maxv=maxv)
+def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts):
+    """One frame as column-strip tiles over the ranks (gqmap_create_tile):
+    RCCL ghost-column and exact-totals exchange every iteration.  Returns the
+    rank's timing and its share of the AEPE sums (interior pixels)."""
+    from gqmap_opticalflow_amd import Engine, comm_unique_id
     eng = Engine(opts, I1, I2, "mixture", args.precision, device=local, n_tiles=world, tile=rank)
-    if world > 1:
-        uid = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        eng.attach_rccl(uid[0])
-    eng.init_state(seed=1)
-    if args.warmup:
-        eng.run(args.warmup)
-    eng.init_state(seed=0)
-    barrier()
-    t0 = time.perf_counter()
-    done, total_ms, kernel_ms = eng.run_timed(args.steps)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    mp = eng.map()
-    col0, col1 = eng.col0, eng.col1
-    eng.close()
+    try:
+        if world > 1:
+            uid = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            eng.attach_rccl(uid[0])
+        eng.init_state(seed=1)
+        if args.warmup:
+            eng.run(args.warmup)
+        eng.init_state(seed=0)  # timed steps are iterations 1..steps of the solve
+        barrier()
+        t0 = time.perf_counter()
+        done, total_ms, kernel_ms = eng.run_timed(args.steps)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if done != args.steps:
+            raise RuntimeError(f"rank {rank}: solver stopped after {done}/{args.steps} iterations")
+        mp = eng.map()
+        col0, col1 = eng.col0, eng.col1
+    finally:
+        eng.close()
     Mo, No = I1.shape
-    # AEPE over this rank's strip (interior), combined on rank 0 as a pixel-weighted mean
+    # AEPE of gqmap_gpu_mixture.m:63-64 over this rank's strip of the interior
     sl = (slice(1, Mo - 1), slice(max(col0, 1), min(col1, No - 1)))
     f = mp.copy()
     f[unk] = 0
     e = np.sqrt(((flo[sl] - f[sl]) ** 2).sum(axis=2))
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, pixels=Mo * No, nodes=Mo * (col1 - col0),
-                err_sum=float(e.sum()), err_n=int(e.size), Mo=Mo, No=No, I1=I1, I2=I2, opts=opts,
-                workload=f"C5: RubberWhale upsampled 4x ({No}x{Mo}, bicubic imresize, uint8-rounded as "
-                         f"imresize(imread(..)) gives), mixture L=1 K=9, "
-                         f"{world} column-strip tile(s), RCCL ghost-column + totals exchange per iteration, "
-                         f"its={args.steps}")
+                err_sum=float(e.sum()), err_n=int(e.size))
+
+
+def run_tiled(args, rank, world, local, barrier, dist, names, scale, label):
+    """C5 (the eight pairs of legacy/optical_flow_temp.m:3 upsampled 4x) or
+    the tiled C2 mode: each pair in turn split over all ranks; the timed
+    region is the sum of the pairs' timed solves (frames resident in HBM)."""
+    from gqmap_opticalflow_amd import flow_to_color, flowio
+    tot = dict(elapsed=0.0, kernel_ms=0.0, pixels=0, nodes=0, pix_its=0, max_nodes=0)
+    per_pair, ref = [], None
+    for name in names:
+        I1, I2, gt = flowio.load_pair_scaled(name, scale, device=local)
+        _, flo, (minu, maxu, minv, maxv), unk = flow_to_color(gt, device=local)
+        opts = dict(its=args.steps, K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdas=5.0, lambdad=1.0,
+                    minu=minu, maxu=maxu, minv=minv, maxv=maxv)
+        r = tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
+        Mo, No = I1.shape
+        for k in ("elapsed", "kernel_ms", "pixels", "nodes"):
+            tot[k] += r[k]
+        tot["pix_its"] += Mo * No * args.steps
+        per_pair.append(dict(name=name, size=f"{No}x{Mo}", err_sum=r["err_sum"], err_n=r["err_n"],
+                             elapsed=r["elapsed"]))
+        if ref is None:
+            ref = (I1, I2, opts)
+    I1, I2, opts = ref
+    desc = ", ".join(f"{p['name']} {p['size']}" for p in per_pair)
+    return dict(tot, per_pair=per_pair, I1=I1, I2=I2, opts=opts, Mo=I1.shape[0], No=I1.shape[1],
+                workload=f"{label}: {len(names)} pair(s) ({desc}), "
+                         + (f"bicubic imresize x{scale:g} of the uint8 RGB frames then rgb2gray "
+                            f"(imresize(imread(..),scale), optical_flow_temp.m:7-8), GT x{scale:g} in size and "
+                            f"value; " if scale != 1 else "")
+                         + f"mixture L=1 K=9, each pair as {world} column-strip tile(s) with RCCL ghost-column + "
+                           f"totals exchange per iteration, its={args.steps} per pair, pairs run in turn")
 
 
 def main():
@@ -272,6 +355,8 @@ def main():
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"))
     ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c4", "c5"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tiled", action="store_true",
+                    help="c2: strong scaling -- the RubberWhale pair split into column strips over the ranks")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = DEFAULT_STEPS[args.config]
@@ -303,7 +388,14 @@ def main():
         torch.cuda.synchronize()
 
     cfg = args.config
-    if cfg == "c2":
+    tiled = cfg == "c5" or (cfg == "c2" and args.tiled)
+    if tiled:
+        if cfg == "c5":
+            r = run_tiled(args, rank, world, local, barrier, dist, C5_PAIRS, 4.0, "C5")
+        else:
+            r = run_tiled(args, rank, world, local, barrier, dist, ("rubberwhale",), 1.0, "C2 tiled")
+        engine, L, K = "mixture", 1, 9
+    elif cfg == "c2":
         r = run_engine_config(args, rank, world, local, barrier, "mixture", PAIRS if world > 1 else PAIRS[:1],
                               1, 9, {}, "C2")
         engine, L, K = "mixture", 1, 9
@@ -317,9 +409,6 @@ def main():
     elif cfg == "c1":
         r = run_c1(args, rank, world, local, barrier)
         engine, L, K = "legacy", 1, 9
-    else:
-        r = run_c5(args, rank, world, local, barrier, dist)
-        engine, L, K = "mixture", 1, 9
 
     elapsed = r["elapsed"]
     kernel_ms = r.get("kernel_ms", 0.0)
@@ -328,12 +417,16 @@ def main():
         t = torch.tensor([elapsed, kernel_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = t.tolist()
-        if cfg == "c5":
-            s = torch.tensor([r["err_sum"], r["err_n"]], device=dev, dtype=torch.float64)
-            dist.all_reduce(s)
-            r["aepe"] = s[0].item() / s[1].item()
-    elif cfg == "c5":
-        r["aepe"] = r["err_sum"] / r["err_n"]
+    if tiled:  # per pair: the ranks' strip sums -> the pair's AEPE; then the mean over pairs
+        sums = [p["err_sum"] for p in r["per_pair"]] + [p["err_n"] for p in r["per_pair"]]
+        if dist is not None:
+            t = torch.tensor(sums, device=dev, dtype=torch.float64)
+            dist.all_reduce(t)
+            sums = t.tolist()
+        n = len(r["per_pair"])
+        for i, p in enumerate(r["per_pair"]):
+            p["aepe"] = sums[i] / sums[n + i]
+        r["aepe"] = float(np.mean([p["aepe"] for p in r["per_pair"]]))
 
     if rank == 0:
         if cfg == "c3":
@@ -342,8 +435,8 @@ def main():
         elif cfg == "c1":
             units = world * r["pixels"] * r["its"]
             parallel = f"frame-parallel x{world}"
-        elif cfg == "c5":
-            units = r["pixels"] * args.steps
+        elif tiled:
+            units = r["pix_its"]
             parallel = f"column-strip tiles x{world} (RCCL halo)"
         else:
             units = world * r["pixels"] * args.steps
@@ -351,7 +444,7 @@ def main():
         out = {
             "metric": METRIC, "value": units / elapsed / 1e9, "unit": "Gpixel-iter/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "strong" if cfg == "c5" else "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "strong" if tiled else "weak", "vs_baseline": None,
             "dtype": "f64" if args.precision == "fp64" else "f32",
             "data": "Middlebury frame10/11 + flow10.flo (real frames, in-repo data/middlebury)"
                     + ("; upsampled 4x on the device" if cfg == "c5" else ""),
@@ -375,15 +468,20 @@ def main():
                                "algorithmic_bytes_per_node_iter": algorithmic_bytes_per_node("ctf", 1, Sb)}
             out["config"]["its_per_level"] = r["its"]
         else:
-            kern_avg_s = kernel_ms / args.steps / 1e3
-            nodes = r["nodes"]
+            # tiled: the kernel mean over all pairs' launches; nodes = the
+            # rank's average share of a pair's grid
+            nsteps = args.steps * (len(r["per_pair"]) if tiled else 1)
+            kern_avg_s = kernel_ms / nsteps / 1e3
+            nodes = r["nodes"] / (len(r["per_pair"]) if tiled else 1)
             out["roofline"] = roofline(engine, L, K, nodes, args.precision, kern_avg_s, cfg,
                                        r.get("kernel", "gq::k_iter"))
+        if tiled:
+            out["per_pair"] = [{k: p[k] for k in ("name", "size", "aepe", "elapsed")} for p in r["per_pair"]]
         if not args.no_cpu_baseline and cfg == "c1":
             out["cpu_baseline"] = cpu_baseline_c1(r["flow"], r["opts"])
         elif not args.no_cpu_baseline:
             lab = {"c2": "RubberWhale", "c3": "Grove3 full-resolution level", "c4": "Urban3",
-                   "c5": "RubberWhale x4"}[cfg]
+                   "c5": "Urban3 x4"}[cfg]
             I1c, I2c, oc = r["I1"], r["I2"], r["opts"]
             if cfg == "c5":  # bounded sample: a 388x584 window of the upsampled frame
                 I1c, I2c = (np.asfortranarray(a[600:988, 900:1484]) for a in (I1c, I2c))

@@ -22,7 +22,7 @@ LMAX, KMAX = 8, 16
 
 # Every entry point declared in include/gqmap.h (checked by tests/test_abi.py).
 EXPORTS = (
-    "gqmap_options_default", "gqmap_create", "gqmap_set_images", "gqmap_init_state",
+    "gqmap_options_default", "gqmap_options_alpha_mode", "gqmap_create", "gqmap_set_images", "gqmap_init_state",
     "gqmap_set_state", "gqmap_get_state", "gqmap_run", "gqmap_run_timed", "gqmap_get_info",
     "gqmap_get_map", "gqmap_log_p", "gqmap_synchronize", "gqmap_destroy", "gqmap_projsplx",
     "gqmap_mixture_map", "gqmap_flow_to_color", "gqmap_gauss_hermite", "gqmap_rand_uniform",
@@ -30,7 +30,7 @@ EXPORTS = (
     "gqmap_warp_image", "gqmap_ctf_create", "gqmap_ctf_set_images", "gqmap_ctf_run",
     "gqmap_ctf_get_level", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
     "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run",
-    "gqmap_cpu_options_default", "gqmap_cpu_run", "gqmap_read_flo", "gqmap_write_flo", "gqmap_aepe",
+    "gqmap_cpu_options_default", "gqmap_cpu_run", "gqmap_cpu_release", "gqmap_read_flo", "gqmap_write_flo", "gqmap_aepe",
 )
 CTF_MAX_LEVELS = 8
 
@@ -92,6 +92,7 @@ def load():
     vp = C.c_void_p
     sig = {
         "gqmap_options_default": (None, [P(GqmapOptions), C.c_int]),
+        "gqmap_options_alpha_mode": (C.c_int, [P(GqmapOptions), C.c_int]),
         "gqmap_create": (C.c_int, [P(vp), P(GqmapOptions), C.c_int]),
         "gqmap_set_images": (C.c_int, [vp, _D, _D, C.c_int, C.c_int]),
         "gqmap_init_state": (C.c_int, [vp, C.c_uint64]),
@@ -125,6 +126,7 @@ def load():
         "gqmap_tile_attach_rccl": (C.c_int, [vp, u8]),
         "gqmap_tile_group_run": (C.c_int, [P(vp), C.c_int, C.c_int, P(C.c_int), _D]),
         "gqmap_cpu_options_default": (None, [P(GqmapCpuOptions)]),
+        "gqmap_cpu_release": (C.c_int, []),
         "gqmap_read_flo": (C.c_int, [C.c_char_p, P(C.c_int), P(C.c_int), _D]),
         "gqmap_write_flo": (C.c_int, [C.c_char_p, _D, C.c_int, C.c_int]),
         "gqmap_aepe": (C.c_int, [_D, _D, u8, C.c_int, C.c_int, C.c_int, _D]),

@@ -1635,6 +1635,27 @@ void gqmap_options_default(gqmap_options *o, int engine)
     o->sig_init = -1.0;  /* sigma = rand + (max-min) (gqmap_gpu_mixture.m:21-22) */
 }
 
+gqmap_status gqmap_options_alpha_mode(gqmap_options *o, int mode)
+{
+    clear_error();
+    GQ_CHECK(o, GQMAP_ERR_INVALID_ARG, "gqmap_options_alpha_mode: null options");
+    GQ_CHECK(mode == GQMAP_ALPHA_SOFTMAX || mode == GQMAP_ALPHA_PROJSPLX, GQMAP_ERR_INVALID_ARG,
+             "unknown alpha mode %d", mode);
+    o->alpha_mode = mode;
+    if (o->engine == GQMAP_ENGINE_CTF) return GQMAP_OK;  // L == 1: no alpha update
+    const bool sup = o->engine == GQMAP_ENGINE_SUPER;
+    if (mode == GQMAP_ALPHA_PROJSPLX && sup) {
+        // gqmap_gpuSuper_mix_entropy.m:48 (commented): it>200, step*1E-6
+        o->alpha_start = 200;
+        o->alpha_lr = 1e-6;
+    } else {
+        // updateAlpha (:50, :83 / super :49, :82) and gqmap_gpu_mixture.m:49: it>500, 1E-7
+        o->alpha_start = 500;
+        o->alpha_lr = 1e-7;
+    }
+    return GQMAP_OK;
+}
+
 gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
 {
     clear_error();
@@ -2159,6 +2180,15 @@ gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n, int n_iter, int *n_d
     }
     Ctl h0;
     gqmap_status s = read_ctl(t0, &h0);
+    // The device trace is a ring of TRACE_CAP iterations: copy out what ran
+    // since the last drain at every stop check (every 64 iterations) and at the end.
+    int fetched = 0;
+    auto drain = [&](const Ctl &h) -> gqmap_status {
+        const int ran = h.it - h0.it;
+        const gqmap_status r = fetch_trace(t0, h0.it + fetched, ran - fetched, trace ? trace + 3 * (size_t)fetched : nullptr);
+        fetched = ran;
+        return r;
+    };
     const size_t hb = (size_t)NPLANES * t0->L * t0->M * t0->rsz;
     for (int i = 0; i < n_iter && s == GQMAP_OK; ++i) {
         for (int t = 0; t < n; ++t) launch_iter(tiles[t]);
@@ -2184,19 +2214,19 @@ gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n, int n_iter, int *n_d
         }
         for (int t = 0; t < n; ++t) launch_finalize(tiles[t]);
         if (hipGetLastError() != hipSuccess) s = GQMAP_ERR_HIP;
-        if (i % 64 == 63 && s == GQMAP_OK) {  // stop test (and bounded queue depth)
+        if (i % 64 == 63 && s == GQMAP_OK) {  // stop test, bounded queue depth, trace drain
             Ctl h;
-            if ((s = read_ctl(t0, &h)) == GQMAP_OK && h.stop) break;
+            if ((s = read_ctl(t0, &h)) == GQMAP_OK) s = drain(h);
+            if (s == GQMAP_OK && h.stop) break;
         }
     }
     if (s != GQMAP_OK && !gqmap_last_error()[0]) set_error("gqmap_tile_group_run: HIP launch failed");
     Ctl h;
     if (s == GQMAP_OK) s = read_ctl(t0, &h);
+    if (s == GQMAP_OK) s = drain(h);
     for (int t = 0; t < n; ++t) tiles[t]->stream = saved[t];
     if (s != GQMAP_OK) return s;
-    const int ran = h.it - h0.it;
-    if ((s = fetch_trace(t0, h0.it, std::min(ran, TRACE_CAP), trace)) != GQMAP_OK) return s;
-    if (n_done) *n_done = ran;
+    if (n_done) *n_done = h.it - h0.it;
     return GQMAP_OK;
 }
 

@@ -143,31 +143,31 @@ __global__ void k_legacy_update(LgParams P)
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int it = P.ctl[0];
     unsigned long long *slot = P.maxbits + 3 * (size_t)(it - 1);
-    if (t >= (int64_t)M * N * 2) {  // still takes part in the block maximum
-        block_amax3(slot, 0, 0, 0);
-        return;
-    }
-    const int m = (int)(t % M), n = (int)((t / M) % N), l = (int)(t / ((int64_t)M * N));
-    const double *de = P.dedge;
-    // (:58-59) dmu = dnode + sum_j dedge(:,:,j,1) + (dedge(m+1,n,1,2) + dedge(m,n+1,2,2))
-    double a = P.dnode[i4(M, N, m, n, 0, l)] + (de[i5(M, N, m, n, 0, 0, l)] + de[i5(M, N, m, n, 1, 0, l)]);
-    double b = P.dnode[i4(M, N, m, n, 1, l)] + (de[i5(M, N, m, n, 0, 2, l)] + de[i5(M, N, m, n, 1, 2, l)]);
-    const double nu = m + 1 < M ? de[i5(M, N, m + 1, n, 0, 1, l)] : 0.0;
-    const double nl = n + 1 < N ? de[i5(M, N, m, n + 1, 1, 1, l)] : 0.0;
-    const double su = m + 1 < M ? de[i5(M, N, m + 1, n, 0, 3, l)] : 0.0;
-    const double sl = n + 1 < N ? de[i5(M, N, m, n + 1, 1, 3, l)] : 0.0;
-    a = a + (nu + nl);
-    b = b + (su + sl);
-    const double step = P.step0 / (1 + it / P.step_decay);  // (:62)
-    const size_t q = i3(M, N, m, n, l);
-    P.mu[q] = P.mu[q] + a * step;               // (:63)
-    P.sigma[q] = fabs(P.sigma[q] + b * step);   // (:64)
-    double mp = 0;
-    for (int j = 0; j < 2; ++j) {               // (:65)
-        const double d = de[i5(M, N, m, n, j, 4, l)];
-        mp = fmax(mp, fabs(d));
-        const size_t r = i4(M, N, m, n, j, l);
-        P.rou[r] = fmax(fmin(P.rou[r] + d * step, P.corr), -P.corr);
+    // Threads past the last node contribute zeros: every thread reaches the
+    // single block_amax3 call below (its barrier is never on a divergent path).
+    double a = 0, b = 0, mp = 0;
+    if (t < (int64_t)M * N * 2) {
+        const int m = (int)(t % M), n = (int)((t / M) % N), l = (int)(t / ((int64_t)M * N));
+        const double *de = P.dedge;
+        // (:58-59) dmu = dnode + sum_j dedge(:,:,j,1) + (dedge(m+1,n,1,2) + dedge(m,n+1,2,2))
+        a = P.dnode[i4(M, N, m, n, 0, l)] + (de[i5(M, N, m, n, 0, 0, l)] + de[i5(M, N, m, n, 1, 0, l)]);
+        b = P.dnode[i4(M, N, m, n, 1, l)] + (de[i5(M, N, m, n, 0, 2, l)] + de[i5(M, N, m, n, 1, 2, l)]);
+        const double nu = m + 1 < M ? de[i5(M, N, m + 1, n, 0, 1, l)] : 0.0;
+        const double nl = n + 1 < N ? de[i5(M, N, m, n + 1, 1, 1, l)] : 0.0;
+        const double su = m + 1 < M ? de[i5(M, N, m + 1, n, 0, 3, l)] : 0.0;
+        const double sl = n + 1 < N ? de[i5(M, N, m, n + 1, 1, 3, l)] : 0.0;
+        a = a + (nu + nl);
+        b = b + (su + sl);
+        const double step = P.step0 / (1 + it / P.step_decay);  // (:62)
+        const size_t q = i3(M, N, m, n, l);
+        P.mu[q] = P.mu[q] + a * step;               // (:63)
+        P.sigma[q] = fabs(P.sigma[q] + b * step);   // (:64)
+        for (int j = 0; j < 2; ++j) {               // (:65)
+            const double d = de[i5(M, N, m, n, j, 4, l)];
+            mp = fmax(mp, fabs(d));
+            const size_t r = i4(M, N, m, n, j, l);
+            P.rou[r] = fmax(fmin(P.rou[r] + d * step, P.corr), -P.corr);
+        }
     }
     block_amax3(slot, abits(a), abits(b), abits(mp));
 }
@@ -195,6 +195,25 @@ __global__ void k_legacy_ctl(LgParams P)
     if (it + 1 > P.its || (it + 1 > P.min_its && mx[0] < P.tor)) P.ctl[1] = 1;  // (:70)
 }
 
+// One device arena per host thread and device, kept across calls: the nine
+// buffers (~300 B per pixel) of gqmap_cpu_run are carved from it, so a
+// repeated call pays no hipMalloc/hipFree (they dominated a 50-iteration
+// call's wall clock).  gqmap_cpu_release() frees the calling thread's arenas.
+struct Arena {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t release()
+    {
+        void *q = p;
+        p = nullptr;  // cleared before the result is checked: never a dangling pointer
+        cap = 0;
+        return q ? hipFree(q) : hipSuccess;
+    }
+    ~Arena() { (void)release(); }
+};
+constexpr int kArenaDev = 64;
+thread_local Arena g_arenas[kArenaDev];
+
 }  // namespace
 }  // namespace gq
 
@@ -215,6 +234,23 @@ void gqmap_cpu_options_default(gqmap_cpu_options *o)
     o->corr_tor = 0.97;      // (:65)
     o->tor = 1e-3;           // (:12)
     o->min_its = 100;        // (:70)
+}
+
+gqmap_status gqmap_cpu_release(void)
+{
+    clear_error();
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    hipError_t first = hipSuccess;
+    for (int d = 0; d < kArenaDev; ++d) {
+        if (!g_arenas[d].p) continue;
+        if (hipSetDevice(d) != hipSuccess) continue;
+        const hipError_t e = g_arenas[d].release();
+        if (first == hipSuccess) first = e;
+    }
+    if (cur >= 0) (void)hipSetDevice(cur);
+    GQ_HIP(first);
+    return GQMAP_OK;
 }
 
 gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int N, const double *sigma0,
@@ -249,14 +285,7 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     // pays no hipMalloc/hipFree (they dominated a 50-iteration call's wall clock).
     struct Buf { void *p = nullptr; };
     Buf bflow, bmu, bsg, brou, bdn, bde, bmax, bctl, btr;
-    struct Arena {
-        void *p = nullptr;
-        size_t cap = 0;
-        ~Arena() { if (p) (void)hipFree(p); }
-    };
-    constexpr int kMaxDev = 64;
-    thread_local Arena arenas[kMaxDev];
-    GQ_CHECK(device < kMaxDev, GQMAP_ERR_INVALID_ARG, "device %d >= %d", device, kMaxDev);
+    GQ_CHECK(device < kArenaDev, GQMAP_ERR_INVALID_ARG, "device %d >= %d", device, kArenaDev);
     const size_t sizes[9] = {sizeof(double) * 2 * MN, sizeof(double) * 2 * MN, sizeof(double) * 2 * MN,
                              sizeof(double) * 4 * MN, sizeof(double) * 4 * MN, sizeof(double) * 20 * MN,
                              sizeof(unsigned long long) * 3 * (size_t)o->its, sizeof(int) * 4,
@@ -264,10 +293,11 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     Buf *bufs[9] = {&bflow, &bmu, &bsg, &brou, &bdn, &bde, &bmax, &bctl, &btr};
     size_t need = 0;
     for (size_t sz : sizes) need += (sz + 255) & ~(size_t)255;
-    Arena &A = arenas[device];
-    if (A.cap < need) {
-        if (A.p) GQ_HIP(hipFree(A.p));
-        A.p = nullptr; A.cap = 0;
+    Arena &A = g_arenas[device];
+    // Regrow when too small, shrink when a call needs under a quarter of it
+    // (a large call does not pin its footprint for the thread's lifetime).
+    if (A.cap < need || need < A.cap / 4) {
+        GQ_HIP(A.release());
         const size_t cap = need + need / 8;  // headroom: a longer run reuses it
         GQ_HIP(hipMalloc(&A.p, cap));
         A.cap = cap;

@@ -40,6 +40,9 @@ def make_options(options: dict, engine: str = "mixture", precision: str = "fp64"
     for k in ("temperature", "drate", "epsn", "lambdad", "lambdas", "minu", "maxu", "minv", "maxv"):
         if k in options:
             setattr(o, k, float(options[k]))
+    o.engine = ENGINES[engine]
+    if "alpha_mode" in options:  # the mode's reference alpha_start / alpha_lr, unless given below
+        check(lib.gqmap_options_alpha_mode(C.byref(o), int(options["alpha_mode"])), "alpha_mode")
     for k in KNOBS:
         if k in options:
             cur = getattr(o, k)

@@ -118,3 +118,39 @@ def load_preprocessed(name: str, root: str = DATA_DIR):
     pair = name if os.path.isdir(os.path.join(root, name)) else name.lower()
     gt = read_flow_file(os.path.join(root, pair, "flow10.flo"))
     return np.asfortranarray(I1, dtype=np.float64), np.asfortranarray(I2, dtype=np.float64), gt
+
+
+# The eight ground-truth pairs of legacy/optical_flow_temp.m:3 (BASELINE config C5)
+C5_PAIRS = ("Urban3", "Grove3", "Urban2", "Venus", "Dimetrodon", "rubberwhale", "Grove2", "Hydrangea")
+
+
+def to_uint8(a: np.ndarray) -> np.ndarray:
+    """MATLAB's double -> uint8 conversion (what imresize returns for uint8
+    input): round half away from zero, saturate to [0, 255]."""
+    return np.clip(np.sign(a) * np.floor(np.abs(a) + 0.5), 0, 255).astype(np.uint8)
+
+
+def load_pair_scaled(name: str, scale: float, device: int = 0, root: str = DATA_DIR):
+    """optical_flow_temp.m:7-8 / optical_flowSuper.m:8-11 at any scale:
+    img = imresize(imread(frame), scale) on the uint8 RGB frame (bicubic,
+    resampled on the device, rounded back to uint8), then double(rgb2gray(img)).
+    The GT flow is resized to the frame (nearest, each pixel repeated) and
+    multiplied by the scale -- the reference keeps its GT at scale 1, so this
+    part is this build's choice for an upsampled benchmark (unknown entries
+    stay > 1e9).  Returns I1, I2 (double) and the GT flow."""
+    from .ops import imresize
+    d = os.path.join(root, name)
+    frames = []
+    for f in ("frame10.png", "frame11.png"):
+        rgb = imread(os.path.join(d, f))
+        if scale != 1:
+            rgb = to_uint8(imresize(rgb.astype(np.float64), scale, device=device))
+        frames.append(np.asfortranarray(rgb2gray(rgb).astype(np.float64)))
+    gt = read_flow_file(os.path.join(d, "flow10.flo"))
+    if scale != 1:
+        r = int(round(scale))
+        if r != scale or r < 1:
+            raise ValueError("GT resizing supports integer upscaling only")
+        gt = np.asfortranarray(np.repeat(np.repeat(gt, r, axis=0), r, axis=1) * float(scale))
+        gt = gt[:frames[0].shape[0], :frames[0].shape[1]]
+    return frames[0], frames[1], gt

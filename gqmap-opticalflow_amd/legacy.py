@@ -36,9 +36,16 @@ def gqmap_cpu(options: dict, flow, *, sigma0=None, seed: int = 0, device: int = 
     trace = np.zeros((max(o.its, 1), 3))
     done = C.c_int(0)
     sg = None if sigma0 is None else f64(sigma0)
+    if sg is not None and sg.shape != (M, N, 2):
+        raise ValueError(f"sigma0 must be {M} x {N} x 2 like flow, got {sg.shape}")
     check(_lib.load().gqmap_cpu_run(C.byref(o), dptr(flow), M, N, dptr(sg) if sg is not None else None,
                                     C.c_uint64(seed), dptr(mu), dptr(sigma), dptr(rou), dptr(trace),
                                     C.byref(done), device), "gqmap_cpu_run")
     if return_trace:
         return mu, sigma, rou, trace[:done.value]
     return mu, sigma, rou
+
+
+def release() -> None:
+    """Free the calling thread's device arenas of gqmap_cpu (gqmap_cpu_release)."""
+    check(_lib.load().gqmap_cpu_release(), "gqmap_cpu_release")

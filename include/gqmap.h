@@ -115,6 +115,12 @@ typedef struct gqmap_ctx gqmap_ctx;
 
 /* ---- engine (gqmap_gpu_mixture.m / gqmap_gpuSuper_mix_entropy.m) ---- */
 void gqmap_options_default(gqmap_options *opt, int engine);
+/* Select the alpha update and set alpha_start / alpha_lr to the reference
+ * constants of that mode for opt->engine: softmax (updateAlpha) it>500,
+ * 1e-7 (gqmap_gpu_mixture.m:50,83; gqmap_gpuSuper_mix_entropy.m:49,82);
+ * projsplx: mixture it>500, 1e-7 (gqmap_gpu_mixture.m:49), super it>200,
+ * 1e-6 (gqmap_gpuSuper_mix_entropy.m:48).  Call after gqmap_options_default. */
+gqmap_status gqmap_options_alpha_mode(gqmap_options *opt, int mode);
 gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device);
 /* I1,I2: Mo x No doubles (greyscale 0..255).  SUPER needs Mo,No divisible by 4.
  * Builds the cubic-convolution padded copy of I2 (getVV, gqmap_gpu_mixture.m:191). */
@@ -243,6 +249,11 @@ void gqmap_cpu_options_default(gqmap_cpu_options *o);
 gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int N,
                            const double *sigma0, uint64_t seed, double *mu, double *sigma, double *rou,
                            double *trace, int *its_done, int device);
+/* gqmap_cpu_run keeps its device buffers in a per-thread, per-device arena
+ * across calls (a call needing under a quarter of it shrinks it); this frees
+ * the calling thread's arenas now.  Replaces nothing in the reference (the
+ * MATLAB runtime owns its gpuArray pool). */
+gqmap_status gqmap_cpu_release(void);
 
 /* ---- host helpers (no device needed) ---- */
 /* readFlowFile.m: M x N x 2 (flow == NULL: size query). */

@@ -79,6 +79,9 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[])
     o.maxu = field_d(opt, "maxu");
     o.minv = field_d(opt, "minv");
     o.maxv = field_d(opt, "maxv");
+    // optional (not read by the reference): projsplx alpha update (:49 / super :48, commented there)
+    if (mxGetField(opt, 0, "alpha_mode"))
+        fail(gqmap_options_alpha_mode(&o, (int)field_d(opt, "alpha_mode")), "options.alpha_mode");
     const uint64_t seed = (uint64_t)field_d(opt, "seed", false, 0);
     const std::string dir = field_s(opt, "dir");
     const mxArray *tflow = mxGetField(opt, 0, "trueFlow");

@@ -22,8 +22,9 @@
 #define I5(m, n, j, q, l) ((m) + (size_t)M * ((n) + (size_t)N * ((j) + 2 * ((q) + 5 * (size_t)(l)))))
 
 int orc_cpu_run(const orc_cpu_params *P, const double *X, const double *W, const double *flow, int M, int N,
-                double *mu, double *sigma, double *rou, double *trace)
+                double *mu, double *sigma, double *rou, double *trace, int nthreads)
 {
+    if (nthreads <= 0) nthreads = 1;
     const int K = P->K, K2 = K * K;
     const double sq2 = sqrt(2.0);
     /* [XI,XJ] = meshgrid(X); WIWJ = WI.*WJ  (:5-6), k = r + K*c */
@@ -39,7 +40,10 @@ int orc_cpu_run(const orc_cpu_params *P, const double *X, const double *W, const
     double *dmu = malloc(sizeof(double) * (size_t)M * N * 2), *dsg = malloc(sizeof(double) * (size_t)M * N * 2);
     int it = 1, done = 0;
     for (;;) {
-        for (int m = 0; m < M - 1; ++m)           /* parfor m=1:M-1 (:17)  */
+        /* parfor m=1:M-1 (:17): rows are independent (each writes its own
+         * dnode/dedge entries), so any thread count gives the same bits */
+#pragma omp parallel for num_threads(nthreads) schedule(static)
+        for (int m = 0; m < M - 1; ++m)
             for (int n = 0; n < N - 1; ++n) {     /* for n=1:N-1   (:18)  */
                 for (int l = 0; l < 2; ++l) {     /* (:20-26) */
                     double du = 0, dsum = 0;

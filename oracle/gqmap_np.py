@@ -100,8 +100,10 @@ class Engine:
         self.sig_hi = float(opts.get("sig_hi", 25.0 if self.sup else 23.0))
         self.sig_lo = float(opts.get("sig_lo", 0.01))
         self.corr = float(opts.get("corr_tor", 1 - 1e-5))
-        self.alpha_start = int(opts.get("alpha_start", 500))
-        self.alpha_lr = float(opts.get("alpha_lr", 1e-7))
+        # projsplx on the super engine: it>200, 1E-6 (gqmap_gpuSuper_mix_entropy.m:48)
+        proj_sup = self.sup and int(opts.get("alpha_mode", 0)) == 1
+        self.alpha_start = int(opts.get("alpha_start", 200 if proj_sup else 500))
+        self.alpha_lr = float(opts.get("alpha_lr", 1e-6 if proj_sup else 1e-7))
         self.t_every = int(opts.get("t_decay_every", 500 if self.sup else 0))
         self.t_min = float(opts.get("t_min", 0.001))
 

@@ -114,7 +114,7 @@ typedef struct {
  * the result on exit; trace[3*i] = max|dmu|, max|dsigma|, max|drou| of
  * iteration i+1.  Returns the number of iterations run. */
 int orc_cpu_run(const orc_cpu_params *P, const double *X, const double *W, const double *flow, int M, int N,
-                double *mu, double *sigma, double *rou, double *trace);
+                double *mu, double *sigma, double *rou, double *trace, int nthreads);
 
 #ifdef __cplusplus
 }

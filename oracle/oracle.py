@@ -118,8 +118,11 @@ def make_params(opts: dict, Mo: int, No: int) -> OrcParams:
     p.sig_hi = float(opts.get("sig_hi", 25.0 if sup else 23.0))
     p.corr_tor = float(opts.get("corr_tor", 1 - 1e-5))
     p.alpha_mode = int(opts.get("alpha_mode", 0))
-    p.alpha_start = int(opts.get("alpha_start", 500))
-    p.alpha_lr = float(opts.get("alpha_lr", 1e-7))
+    # reference constants of the alpha update: projsplx on the super engine
+    # it>200, 1E-6 (gqmap_gpuSuper_mix_entropy.m:48), otherwise it>500, 1E-7
+    proj_sup = sup and p.alpha_mode == 1
+    p.alpha_start = int(opts.get("alpha_start", 200 if proj_sup else 500))
+    p.alpha_lr = float(opts.get("alpha_lr", 1e-6 if proj_sup else 1e-7))
     p.tor = float(opts.get("tor", 1e-4))
     p.ctf = int(eng == "ctf")
     p.sig_step = float(opts.get("sig_step", 1.0))
@@ -411,7 +414,7 @@ def cpu_params(opts: dict) -> OrcCpuParams:
     return p
 
 
-def cpu_run(opts: dict, flow, sigma0, X, W):
+def cpu_run(opts: dict, flow, sigma0, X, W, nthreads: int = 1):
     """legacy/gqmap_cpu.m from mu = flow, sigma = sigma0, rou = 0.
     Returns (mu, sigma, rou, trace[its_done, 3])."""
     flow = _f64(flow)
@@ -424,5 +427,5 @@ def cpu_run(opts: dict, flow, sigma0, X, W):
     X, W = _f64(np.asarray(X, dtype=np.float64)), _f64(np.asarray(W, dtype=np.float64))
     f = lib().orc_cpu_run
     f.restype = C.c_int
-    done = f(C.byref(p), _p(X), _p(W), _p(flow), M, N, _p(mu), _p(sigma), _p(rou), _p(trace))
+    done = f(C.byref(p), _p(X), _p(W), _p(flow), M, N, _p(mu), _p(sigma), _p(rou), _p(trace), int(nthreads))
     return mu, sigma, rou, trace[:done].copy()

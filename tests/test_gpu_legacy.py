@@ -42,3 +42,26 @@ def test_legacy_c1_dimetrodon_50_iterations():
     np.testing.assert_array_equal(tr, r[3])
     e = np.sqrt(((mu - flo) ** 2).sum(axis=2))[~unk].mean()
     print(f"C1: {tr.shape[0]} its, mean |mu - flow| {e:.4f}, last max|dmu| {tr[-1, 0]:.3e}")
+
+
+@pytest.mark.parametrize("shape", [(37, 41), (5, 7), (61, 3)])
+def test_legacy_ragged_sizes_bit_exact(shape):
+    """2*M*N not a multiple of 64 (the last workgroup of k_legacy_update has
+    idle threads that still take part in the block maximum): bit-exact vs the
+    C restatement, traces (the running maxima) included."""
+    from gqmap_opticalflow_amd import gauss_hermite, gqmap_cpu, legacy
+    from oracle import oracle
+    M, N = shape
+    assert (2 * M * N) % 64 != 0
+    rng = np.random.default_rng(7)
+    flow = np.asfortranarray(rng.normal(0, 3, (M, N, 2)))
+    sg0 = np.asfortranarray(rng.uniform(0, 1, (M, N, 2)) + 2)
+    o = dict(its=120, K=9, var=1.0, gama=1.0, dta=np.inf, min_its=100, tor=1e-3)
+    X, W = gauss_hermite(9)
+    ref = oracle.cpu_run(o, flow, sg0, X, W)
+    got = gqmap_cpu(o, flow, sigma0=sg0, return_trace=True)
+    for a, b, k in zip(got, ref, ("mu", "sigma", "rou", "trace")):
+        np.testing.assert_array_equal(a, b, err_msg=k)
+    legacy.release()
+    with pytest.raises(ValueError):
+        gqmap_cpu(o, flow, sigma0=sg0[:, :, 0])

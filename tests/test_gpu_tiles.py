@@ -112,3 +112,57 @@ def test_single_rank_rccl_tile_matches_whole_grid():
             np.testing.assert_array_equal(getattr(got, k), getattr(ref, k), err_msg=k)
     finally:
         e.close()
+
+
+def test_c5_frame_eight_tiles_bit_exact_vs_whole_grid():
+    """BASELINE C5's unit of work: one Middlebury pair upsampled 4x
+    (RubberWhale, 1552x2336, imresize of the uint8 RGB frames as
+    optical_flow_temp.m:7-8 does) split into 8 column-strip tiles -- the
+    driver's 8-GPU layout -- on one GPU through the in-process transport:
+    bit-identical to the whole-grid solve after 20 iterations."""
+    from gqmap_opticalflow_amd import Engine, flow_to_color, flowio, tile_group_run
+    I1, I2, gt = flowio.load_pair_scaled("rubberwhale", 4.0)
+    assert I1.shape == (1552, 2336)
+    _, _, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
+    o = dict(K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdad=1.0, lambdas=5.0,
+             minu=minu, maxu=maxu, minv=minv, maxv=maxv)
+    its, n = 20, 8
+    init, ref, tr = _whole(I1, I2, o, "mixture", "fp64", its, seed=0)
+    tiles = [Engine(o, I1, I2, n_tiles=n, tile=t) for t in range(n)]
+    try:
+        for t in tiles:
+            t.init_state(0)
+        done, ttr = tile_group_run(tiles, its)
+        assert done == its
+        np.testing.assert_array_equal(ttr, tr)
+        for t in tiles:
+            s = t.get_state()
+            for k in G.STATE_KEYS[:6]:
+                np.testing.assert_array_equal(getattr(s, k)[:, t.col0:t.col1], getattr(ref, k)[:, t.col0:t.col1],
+                                              err_msg=f"tile {t.tile} {k}")
+    finally:
+        for t in tiles:
+            t.close()
+
+
+def test_tile_group_long_run_trace_drained():
+    """gqmap_tile_group_run copies the device trace ring out every 64
+    iterations: a run longer than the ring (8192) returns every row."""
+    from gqmap_opticalflow_amd import Engine, tile_group_run
+    I1, I2, o = _problem("mixture", 1, 24, 40)
+    its = 8192 + 150
+    with Engine(dict(o, tor=0.0), I1, I2) as e:
+        e.init_state(2)
+        init = e.get_state()
+        done, tr = e.run(its)
+    assert done == its
+    tiles = [Engine(dict(o, tor=0.0), I1, I2, n_tiles=2, tile=t) for t in range(2)]
+    try:
+        for t in tiles:
+            t.set_state(init.copy())
+        done, ttr = tile_group_run(tiles, its)
+        assert done == its and ttr.shape == (its, 3)
+        np.testing.assert_array_equal(ttr, tr)
+    finally:
+        for t in tiles:
+            t.close()

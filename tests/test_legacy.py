@@ -34,3 +34,15 @@ def test_legacy_stop_rule_and_clamps(oracle_lib):
     mu, sg, rou, tr = oracle_lib.cpu_run(dict(its=400, K=5, tor=1e9), flow, sg0, X5, W5)
     assert tr.shape[0] == 100  # stops right after iteration 100
     assert np.abs(rou).max() <= 0.97 and (sg >= 0).all()
+
+
+def test_legacy_oracle_thread_count_invariant(oracle_lib):
+    # parfor over rows (legacy/gqmap_cpu.m:17): the OpenMP row split is exact
+    from gqmap_opticalflow_amd import gauss_hermite
+    d = _load()
+    X, W = gauss_hermite(9)
+    o = dict(its=6, K=9, var=1.0, gama=1.0, dta=2.5)
+    a = oracle_lib.cpu_run(o, d["flow"], d["sigma0"], X, W, nthreads=1)
+    b = oracle_lib.cpu_run(o, d["flow"], d["sigma0"], X, W, nthreads=5)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
