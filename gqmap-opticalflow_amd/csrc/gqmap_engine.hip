@@ -96,6 +96,7 @@ __device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x
 #define GQ_PAIR_UNROLL GQ_PRAGMA_UNROLL(GQ_PAIR_UNROLL_N)
 #define GQ_NODE_UNROLL GQ_PRAGMA_UNROLL(GQ_NODE_UNROLL_N)
 #define GQ_UNROLL_FULL _Pragma("unroll")
+#define GQ_UMUL24(a, b) __umul24((uint32_t)(a), (uint32_t)(b))
 #include "gqmap_math.h"
 
 namespace gq {

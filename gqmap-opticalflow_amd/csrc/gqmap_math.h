@@ -150,56 +150,96 @@ GQ_HD double from_fix(fix128 v)
 template <typename R>
 GQ_HD void keys4(R t, R &w0, R &w1, R &w2, R &w3)
 {
-    // Keys a=-1/2 weights in the x2 form of the reference
+    // Keys a=-1/2 weights in the x2 form of the reference (they sum to 2):
+    //   ((2-t)t-1)t, (3t-5)t^2+2, ((4-3t)t+1)t, (t-1)t^2
+    // as 8 operations on t2 = t^2 and b = 4-3t (every constant an inline
+    // operand or the one scalar -3):
+    //   w0 = t2(2-t) - t,  w1 = (2-t2) - t2 b,  w2 = t2 b + t,  w3 = t2 t - t2
     const R t2 = t * t;
-    w0 = fma(R(2) - t, t, R(-1)) * t;         // ((2-t)t - 1)t
-    w1 = fma(fma(R(3), t, R(-5)), t2, R(2));  // (3t-5)t^2 + 2
-    w2 = fma(fma(R(-3), t, R(4)), t, R(1)) * t;  // ((4-3t)t + 1)t
-    w3 = (t - R(1)) * t2;                     // (t-1)t^2
+    const R b = fma(R(-3), t, R(4));
+    w0 = fma(t2, R(2) - t, -t);
+    w1 = fma(-t2, b, R(2) - t2);
+    w2 = fma(t2, b, t);
+    w3 = fma(t2, t, -t2);
 }
 
+#ifndef GQ_UMUL24  // 24-bit multiply (full rate on the device; both factors < 2^24)
+#define GQ_UMUL24(a, b) ((uint32_t)(a) * (uint32_t)(b))
+#endif
+
+// Pointer `bytes` past the padded frame's base: a frame is < 4 GiB, so every
+// gather is SGPR base + 32-bit VGPR offset (no 64-bit address arithmetic).
+template <typename VP>
+GQ_HD VP byte_ptr(VP VV, uint32_t bytes)
+{
+    return (VP)((const char *)VV + bytes);
+}
+template <typename VP>
+GQ_HD VP elem_ptr(VP VV, uint32_t elem)
+{
+    return byte_ptr(VV, elem * (uint32_t)sizeof(*VV));
+}
+
+// 4 x the Keys interpolation (the reference's (sum of weighted taps)/4 before
+// the /4): callers fold the 1/4 into their next operation, e.g. the residual
+// I - v as fma(v4, -1/4, I) -- v4/4 is exact, so that is I - v bit for bit.
+// o: element offset of the cell's first tap (top-left), M2: column stride.
 template <typename R, typename VP>
-GQ_HD R bicubic_w(VP c, int M2, R s0, R s1, R s2, R s3, R t0, R t1, R t2, R t3)
+GQ_HD R bicubic_w4(VP VV, uint32_t o, uint32_t M2, R s0, R s1, R s2, R s3, R t0, R t1, R t2, R t3)
 {
 #ifdef GQ_ABL_NOGATHER  // timing ablation only: no memory traffic for the taps
     const R a0 = t0 + s1, a1 = t1 * s2, a2 = t2 - s3, a3 = t3 + s0;
-    return fma(s3, a3, fma(s2, a2, fma(s1, a1, s0 * a0))) * R(0.25) + (R)(int64_t)(c - (VP)0) * R(1e-30);
+    return fma(s3, a3, fma(s2, a2, fma(s1, a1, s0 * a0))) + (R)o * R(1e-30);
 #else
     // taps are converted to R exactly (VV storage: double, or float / half when exact)
-    const R v0 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
-    c += M2;
-    const R v1 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
-    c += M2;
-    const R v2 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
-    c += M2;
-    const R v3 = fma(R(c[3]), t3, fma(R(c[2]), t2, fma(R(c[1]), t1, R(c[0]) * t0)));
-    return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0))) * R(0.25);
+    constexpr uint32_t E = (uint32_t)sizeof(*VV);
+#ifdef GQ_ABL_UNIFORM  // timing ablation only: every lane gathers the same cell (one line per load)
+    const uint32_t ob = (o & 1u) * E, cb = M2 * E;
+#else
+    const uint32_t ob = o * E, cb = M2 * E;  // byte offsets: cell, column stride
+#endif
+    const auto c0 = byte_ptr(VV, ob);
+    const R v0 = fma(R(c0[3]), t3, fma(R(c0[2]), t2, fma(R(c0[1]), t1, R(c0[0]) * t0)));
+    const auto c1 = byte_ptr(VV, ob + cb);
+    const R v1 = fma(R(c1[3]), t3, fma(R(c1[2]), t2, fma(R(c1[1]), t1, R(c1[0]) * t0)));
+    const auto c2 = byte_ptr(VV, ob + 2 * cb);
+    const R v2 = fma(R(c2[3]), t3, fma(R(c2[2]), t2, fma(R(c2[1]), t1, R(c2[0]) * t0)));
+    const auto c3 = byte_ptr(VV, ob + 3 * cb);
+    const R v3 = fma(R(c3[3]), t3, fma(R(c3[2]), t2, fma(R(c3[1]), t1, R(c3[0]) * t0)));
+    return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0)));
 #endif
 }
 
-// Keys interpolation in the cell whose first tap is c, at fraction so
-// (columns) / to (rows).
+// 4 x the Keys interpolation in the cell whose first tap is element o, at
+// fraction so (columns) / to (rows).
 template <typename R, typename VP>
-GQ_HD R bicubic_cell(VP c, int M2, R so, R to)
+GQ_HD R bicubic_cell4(VP VV, uint32_t o, uint32_t M2, R so, R to)
 {
     R t0, t1, t2, t3, s0, s1, s2, s3;
     keys4(to, t0, t1, t2, t3);
     keys4(so, s0, s1, s2, s3);
-    return bicubic_w<R>(c, M2, s0, s1, s2, s3, t0, t1, t2, t3);
+    return bicubic_w4<R>(VV, o, M2, s0, s1, s2, s3, t0, t1, t2, t3);
 }
 
-// One axis of sample()'s position arithmetic: 1-based pixel j displaced by
-// x on an axis of n pixels -> 1-based cell ix and fraction fr.
-// fp64: the reference's own arithmetic (X = j + x, clamp to [1, n], floor).
+GQ_HD uint32_t cell_elem(int iy, int ix, int M2) { return (uint32_t)(iy - 1) + GQ_UMUL24(M2, ix - 1); }
+
+// One axis of sample()'s position arithmetic at the absolute 1-based
+// position X on an axis of n pixels -> 1-based cell ix and fraction fr
+// (fp64: the reference's own arithmetic: clamp to [1, n], floor).
 template <bool CLAMP = true>
-GQ_HD void axis_cell(int j, double x, int n, int &ix, double &fr)
+GQ_HD void axis_cell_abs(double X, int n, int &ix, double &fr)
 {
     // min(max(.,1),N) with MATLAB's NaN-ignoring max/min (IEEE maxNum/minNum)
-    double X = (double)j + x;
     if (CLAMP) X = fmin(fmax(X, 1.0), (double)n);
     ix = (int)X;  // X >= 1: truncation == floor
     if (CLAMP) ix = ix > n - 1 ? n - 1 : ix;
     fr = X - (double)ix;
+}
+// 1-based pixel j displaced by x (fp64: X = j + x, the reference's form).
+template <bool CLAMP = true>
+GQ_HD void axis_cell(int j, double x, int n, int &ix, double &fr)
+{
+    axis_cell_abs<CLAMP>((double)j + x, n, ix, fr);
 }
 // fp32: integer + fraction relative to the pixel, so the fractional position
 // keeps full precision at any image size.
@@ -213,18 +253,33 @@ GQ_HD void axis_cell(int j, float x, int n, int &ix, float &fr)
     if (CLAMP && ix > n - 1) { ix = n - 1; fr = 1.f; }
 }
 
-// interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV
-// (axis_cell per axis: fp64 the reference's own position arithmetic).
+// 4 x interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV.
 // CLAMP = false: the caller guarantees 1 <= jj + x1 < No and 1 <= ii + x2 < Mo
 // for this sample, where every clamp is the identity -- same result.
 template <bool CLAMP = true, typename VP, typename R>
-GQ_HD R sample(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+GQ_HD R sample4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 {
     int ix, iy;
     R so, to;
     axis_cell<CLAMP>(jj, x1, No, ix, so);
     axis_cell<CLAMP>(ii, x2, Mo, iy, to);
-    return bicubic_cell<R>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, so, to);
+    return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, so, to);
+}
+// fp64 at absolute 1-based positions X (column), Y (row).
+template <bool CLAMP = true, typename VP>
+GQ_HD double sample4_abs(VP VV, int M2, int Mo, int No, double X, double Y)
+{
+    int ix, iy;
+    double so, to;
+    axis_cell_abs<CLAMP>(X, No, ix, so);
+    axis_cell_abs<CLAMP>(Y, Mo, iy, to);
+    return bicubic_cell4<double>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, so, to);
+}
+// interp2-cubic itself (node_pot's Vq, gqmap_gpu_mixture.m:157-176).
+template <bool CLAMP = true, typename VP, typename R>
+GQ_HD R sample(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+{
+    return sample4<CLAMP>(VV, M2, Mo, No, ii, jj, x1, x2) * R(0.25);
 }
 
 // Coarse-to-fine level data term (legacy/gqmap_ctf.m:10, 96):
@@ -232,9 +287,9 @@ GQ_HD R sample(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 // with I2_cont = interp2(I2,6,'cubic') the 64x-refined cubic table.  A table
 // entry (r, c) is the same Keys interpolation at (1+(c-1)/64, 1+(r-1)/64), so
 // the lookup is sample() at the position rounded to the 1/64 grid -- the
-// 64x table (10 GB at 480x640) is never built.
+// 64x table (10 GB at 480x640) is never built.  Returns 4 x the entry.
 template <typename VP, typename R>
-GQ_HD R sample_ctf(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 {
     const R MM = R(64 * (Mo - 1) + 1), NN = R(64 * (No - 1) + 1);
     const R ry = fmin(fmax(round((((R)ii + x2) - R(1)) * R(64) + R(1)), R(1)), MM);
@@ -243,7 +298,7 @@ GQ_HD R sample_ctf(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
     int ix = (int)Xq, iy = (int)Yq;  // Xq in [1, No]: truncation == floor
     ix = ix > No - 1 ? No - 1 : ix;
     iy = iy > Mo - 1 ? Mo - 1 : iy;
-    return bicubic_cell<R>(VV + (iy - 1) + (int64_t)M2 * (ix - 1), M2, Xq - (R)ix, Yq - (R)iy);
+    return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, Xq - (R)ix, Yq - (R)iy);
 }
 
 // ---------------------------------------------------------------------------
@@ -272,10 +327,11 @@ GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x
         keys4(to, t0, t1, t2, t3);
         keys4(so, s0, s1, s2, s3);
         // window origin: padded row i0 + fy, padded column j0 + fx (0-based)
-        VP c = VV + (i0 + (int)fy) + (int64_t)M2 * (j0 + (int)fx);
+        const uint32_t o = (uint32_t)(i0 + (int)fy) + (uint32_t)M2 * (uint32_t)(j0 + (int)fx);
         R out[4][4];
         GQ_UNROLL_FULL
-        for (int a = 0; a < 7; ++a, c += M2) {
+        for (int a = 0; a < 7; ++a) {
+            const auto c = elem_ptr(VV, o + (uint32_t)(a * M2));
             R v[4];
             GQ_UNROLL_FULL
             for (int di = 0; di < 4; ++di)
@@ -291,12 +347,12 @@ GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x
             }
         }
         for (int q = 0; q < 16; ++q) {
-            const R d = I[q] - out[q >> 2][q & 3] * R(0.25);
+            const R d = fma(out[q >> 2][q & 3], R(-0.25), I[q]);  // I - out/4, bit for bit
             f = f + GQ_SQRT(fma(d, d, eps));
         }
     } else if (sizeof(R) == 4) {
         for (int q = 0; q < 16; ++q) {
-            const R d = I[q] - sample(VV, M2, Mo, No, i0 + (q >> 2) + 1, j0 + (q & 3) + 1, x1, x2);
+            const R d = fma(sample4(VV, M2, Mo, No, i0 + (q >> 2) + 1, j0 + (q & 3) + 1, x1, x2), R(-0.25), I[q]);
             f = f + GQ_SQRT(fma(d, d, eps));
         }
     } else {
@@ -320,9 +376,9 @@ GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x
             keys4(fr, t0, t1, t2, t3);
             GQ_UNROLL_FULL
             for (int dj = 0; dj < 4; ++dj) {
-                const R v = bicubic_w<R>(VV + (iy - 1) + (int64_t)M2 * (ixs[dj] - 1), M2, sw[dj][0], sw[dj][1],
-                                         sw[dj][2], sw[dj][3], t0, t1, t2, t3);
-                const R d = I[4 * di + dj] - v;
+                const R v4 = bicubic_w4<R>(VV, cell_elem(iy, ixs[dj], M2), (uint32_t)M2, sw[dj][0], sw[dj][1],
+                                           sw[dj][2], sw[dj][3], t0, t1, t2, t3);
+                const R d = fma(v4, R(-0.25), I[4 * di + dj]);
                 f = f + GQ_SQRT(fma(d, d, eps));
             }
         }
@@ -530,19 +586,29 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
     Sums<R> S;
     if (ENG != 1) {
         const R I = I1[m + (int64_t)Mo * n];
-        auto f_at = [&](R x1, R x2) {
-            const R v = ENG == 2 ? sample_ctf(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
-                                 : sample<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
-            const R d = I - v;
-            return GQ_SQRT(fma(d, d, eps));
-        };
-        // one point at a time in increasing k (mirror pairs sample far-apart
-        // cells: measured slower for the gathers, unlike the edge sums)
-        GQ_NODE_UNROLL
-        for (int k = k0; k < K2; k += dk) {
-            const R x1 = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], u1));
-            const R x2 = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], u2));
-            S.add(tab, k, f_at(x1, x2));
+        if constexpr (ENG == 0 && sizeof(R) == 8) {
+            // fp64 single-scale: absolute positions X = j + x1 with the pixel
+            // folded into the mean once per node (U1 = u1 + j)
+            const R U1 = u1 + R(n + 1), U2 = u2 + R(m + 1);
+            GQ_NODE_UNROLL
+            for (int k = k0; k < K2; k += dk) {
+                const R X = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], U1));
+                const R Y = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], U2));
+                const R d = fma(sample4_abs<CLAMP>(VV, M2, Mo, No, X, Y), R(-0.25), I);
+                S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+            }
+        } else {
+            // one point at a time in increasing k (mirror pairs sample far-apart
+            // cells: measured slower for the gathers, unlike the edge sums)
+            GQ_NODE_UNROLL
+            for (int k = k0; k < K2; k += dk) {
+                const R x1 = fma(c.ax, tab[k], fma(c.bx, tab[TAB_STRIDE + k], u1));
+                const R x2 = fma(c.ay, tab[k], fma(c.by, tab[TAB_STRIDE + k], u2));
+                const R v4 = ENG == 2 ? sample_ctf4(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
+                                      : sample4<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
+                const R d = fma(v4, R(-0.25), I);
+                S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+            }
         }
     } else {
         // super = sum_{i=top..bottom} sum_{j=left..right} node_pot(x1,x2,i,j): j fastest
