@@ -55,7 +55,20 @@ __device__ __forceinline__ double gq_sqrt_dev(double x)
     d = fma(-g, g, x);
     return fma(d, h, g);
 }
-__device__ __forceinline__ float gq_sqrt_dev(float x) { return __builtin_sqrtf(x); }
+// correctly rounded f32 sqrt for normal x >= 2^-96 (every argument is eps + d^2
+// with eps >= 2^-96 -- gqmap_create checks that for fp32 -- 1 +- p or 1 - p^2):
+// v_sqrt_f32 is within 1 ulp, the neighbour whose residual brackets x wins
+// (LLVM's f32 sequence without its denormal rescaling and inf/zero fix-up:
+// 9 instructions instead of 17, same bits as sqrtf).
+__device__ __forceinline__ float gq_sqrt_dev(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const int si = __float_as_int(s);
+    const float sm = __int_as_float(si - 1), sp = __int_as_float(si + 1);
+    const float rm = fmaf(-sm, s, x), rp = fmaf(-sp, s, x);
+    const float r = rm <= 0.f ? sm : s;
+    return rp > 0.f ? sp : r;
+}
 }  // namespace gq
 
 #define GQ_HD __device__ __forceinline__
@@ -1017,7 +1030,8 @@ __global__ void k_selftest(int fn, const double *in, double *out, int64_t n)
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double x = in[i];
-    out[i] = fn == 0 ? gq_sqrt_dev(x) : fn == 1 ? gq_log(x) : gq_exp(x);
+    out[i] = fn == 0 ? gq_sqrt_dev(x) : fn == 1 ? gq_log(x) : fn == 2 ? gq_exp(x)
+           : (double)gq_sqrt_dev((float)x);  // 3: the f32 sqrt of (float)x
 }
 
 }  // namespace gq
@@ -1669,6 +1683,8 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
     GQ_CHECK(opt->engine == GQMAP_ENGINE_MIXTURE || opt->engine == GQMAP_ENGINE_SUPER ||
                  opt->engine == GQMAP_ENGINE_CTF,
              GQMAP_ERR_INVALID_ARG, "unknown engine %d", opt->engine);
+    GQ_CHECK(opt->precision != GQMAP_FP32 || opt->epsn >= 0x1p-96, GQMAP_ERR_INVALID_ARG,
+             "fp32 needs epsn >= 2^-96 (its sqrt assumes normal arguments), got %g", opt->epsn);
     GQ_CHECK(opt->engine != GQMAP_ENGINE_CTF || opt->L == 1, GQMAP_ERR_INVALID_ARG,
              "the coarse-to-fine engine is single-Gaussian (L=1)");
     GQ_CHECK(opt->precision == GQMAP_FP64 || opt->precision == GQMAP_FP32, GQMAP_ERR_INVALID_ARG,

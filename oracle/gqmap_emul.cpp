@@ -335,5 +335,6 @@ extern "C" int emu_run(const orc_params *P, const double *X, const double *W, co
 extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)
 {
     for (int64_t i = 0; i < n; ++i)
-        out[i] = fn == 0 ? std::sqrt(in[i]) : fn == 1 ? gq_log(in[i]) : gq_exp(in[i]);
+        out[i] = fn == 0 ? std::sqrt(in[i]) : fn == 1 ? gq_log(in[i]) : fn == 2 ? gq_exp(in[i])
+                                                                   : (double)std::sqrt((float)in[i]);
 }

@@ -324,7 +324,11 @@ def test_device_math_matches_host():
     inputs = {0: np.concatenate([rng.uniform(1e-6, 1e3, 200000), 1e-6 + rng.random(50000) ** 4,
                                  1 + rng.uniform(-1, 1, 50000) * (1 - 1e-5)]),
               1: np.exp(rng.uniform(-12, 7, 100000)),
-              2: rng.uniform(-740, 300, 100000)}
+              2: rng.uniform(-740, 300, 100000),
+              # f32 sqrt on the arguments the fp32 engine passes (eps + d^2, 1 +- p, 1 - p^2)
+              3: np.concatenate([np.float32(1e-6) + rng.uniform(0, 1e4, 200000).astype(np.float32) ** 2,
+                                 rng.uniform(1e-5, 2.0, 100000).astype(np.float32),
+                                 np.exp(rng.uniform(-66, 80, 100000)).astype(np.float32)]).astype(np.float64)}
     for fn, x in inputs.items():
         x = np.ascontiguousarray(x)
         out = np.zeros_like(x)
