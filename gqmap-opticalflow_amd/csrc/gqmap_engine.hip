@@ -123,7 +123,6 @@ typedef float vvs_t;
 constexpr int TILE = 16;
 constexpr int BLOCK = TILE * TILE;
 constexpr int TS = TAB_STRIDE;
-constexpr int NTAB = 8;        // xi, xj, w, w*xi, w*xj, w*(xi^2+xj^2), w*(xi^2-xj^2), w*xi*xj
 constexpr int NPLANES = 9;
 constexpr int TRACE_CAP = 8192;
 constexpr int GRAPH_CHUNK = 50;
@@ -167,7 +166,7 @@ struct IterParams {
     const R *__restrict__ I1;   // Mo x No
     R *st0;
     R *st1;
-    const R *__restrict__ tab;  // NTAB x TS
+    const R *__restrict__ tab;  // TS x NTAB, point-major (tab_at)
     Ctl *ctl;
     fix128 *partials;           // nblocks x (NFIX + L)
     int M, N, Mo, No, M2, L, K2;
@@ -484,10 +483,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     using tab_t = std::conditional_t<TAB_LDS, const R *, ctab_t<R>>;
     tab_t tab;
     if constexpr (TAB_LDS) {
-        for (int e = threadIdx.x; e < NTAB * K2; e += BLOCK) {
-            const int r = e / K2, k = e - r * K2;
-            lds.tab[r * TS + k] = P.tab[r * TS + k];
-        }
+        for (int e = threadIdx.x; e < NTAB * K2; e += BLOCK) lds.tab[e] = P.tab[e];
         __syncthreads();
         tab = lds.tab;
     } else {
@@ -1169,7 +1165,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.sig_lo = R(o.sig_lo); P.sig_hi = R(o.sig_hi); P.corr = R(o.corr_tor);
     P.sig_step = R(o.sig_step);
     double xmax = 0;
-    for (int k = 0; k < c->K2; ++k) xmax = std::max(xmax, std::fabs(c->tab_host[k]));
+    for (int k = 0; k < c->K2; ++k) xmax = std::max(xmax, std::fabs(c->tab_host[tab_at(0, k)]));
     P.gh_xmax = R(xmax);
     P.step0 = o.step0; P.step_decay = o.step_decay;
     P.guard = o.guard_a;
@@ -1719,14 +1715,14 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
         for (int r = 0; r < c->K; ++r) {
             const int k = r + c->K * cc;
             const double xi = X[cc], xj = X[r], w = W[cc] * W[r];
-            c->tab_host[0 * TS + k] = xi;
-            c->tab_host[1 * TS + k] = xj;
-            c->tab_host[2 * TS + k] = w;
-            c->tab_host[3 * TS + k] = w * xi;
-            c->tab_host[4 * TS + k] = w * xj;
-            c->tab_host[5 * TS + k] = w * (xi * xi + xj * xj);
-            c->tab_host[6 * TS + k] = w * (xi * xi - xj * xj);
-            c->tab_host[7 * TS + k] = w * (xi * xj);
+            c->tab_host[tab_at(0, k)] = xi;
+            c->tab_host[tab_at(1, k)] = xj;
+            c->tab_host[tab_at(2, k)] = w;
+            c->tab_host[tab_at(3, k)] = w * xi;
+            c->tab_host[tab_at(4, k)] = w * xj;
+            c->tab_host[tab_at(5, k)] = w * (xi * xi + xj * xj);
+            c->tab_host[tab_at(6, k)] = w * (xi * xi - xj * xj);
+            c->tab_host[tab_at(7, k)] = w * (xi * xj);
         }
     gqmap_status st = GQMAP_OK;
     auto fail = [&](gqmap_status s) { gqmap_destroy(c); return s; };

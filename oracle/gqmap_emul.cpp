@@ -90,19 +90,19 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
     const int M = w.M, N = w.N, L = w.L;
     const int64_t MN = w.MN, MNL = w.MNL;
     // quadrature tables exactly as gqmap_create builds them
-    std::vector<double> tabd(8 * TAB_STRIDE, 0.0);
+    std::vector<double> tabd(NTAB * TAB_STRIDE, 0.0);
     for (int cc = 0; cc < P->K; ++cc)
         for (int r = 0; r < P->K; ++r) {
             const int k = r + P->K * cc;
             const double xi = X[cc], xj = X[r], ww = W[cc] * W[r];
-            tabd[0 * TAB_STRIDE + k] = xi;
-            tabd[1 * TAB_STRIDE + k] = xj;
-            tabd[2 * TAB_STRIDE + k] = ww;
-            tabd[3 * TAB_STRIDE + k] = ww * xi;
-            tabd[4 * TAB_STRIDE + k] = ww * xj;
-            tabd[5 * TAB_STRIDE + k] = ww * (xi * xi + xj * xj);
-            tabd[6 * TAB_STRIDE + k] = ww * (xi * xi - xj * xj);
-            tabd[7 * TAB_STRIDE + k] = ww * (xi * xj);
+            tabd[tab_at(0, k)] = xi;
+            tabd[tab_at(1, k)] = xj;
+            tabd[tab_at(2, k)] = ww;
+            tabd[tab_at(3, k)] = ww * xi;
+            tabd[tab_at(4, k)] = ww * xj;
+            tabd[tab_at(5, k)] = ww * (xi * xi + xj * xj);
+            tabd[tab_at(6, k)] = ww * (xi * xi - xj * xj);
+            tabd[tab_at(7, k)] = ww * (xi * xj);
         }
     w.tab.assign(tabd.begin(), tabd.end());
     const size_t nvv = (size_t)(w.Mo + 2) * (w.No + 2), ni = (size_t)w.Mo * w.No;
