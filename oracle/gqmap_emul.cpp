@@ -338,3 +338,6 @@ extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)
         out[i] = fn == 0 ? std::sqrt(in[i]) : fn == 1 ? gq_log(in[i]) : fn == 2 ? gq_exp(in[i])
                                                                    : (double)std::sqrt((float)in[i]);
 }
+
+// the device's deterministic exp as a plain function (orc_set_map_exp)
+extern "C" double emu_gq_exp(double x) { return gq_exp(x); }

@@ -636,12 +636,19 @@ double orc_aepe(const double *tflow, const double *flow, const unsigned char *un
 /* ------------------------------------------------------------------ */
 /* Mixture MAP (findMixMax.m:39-70) with MATLAB fminbnd (Brent)         */
 /* ------------------------------------------------------------------ */
+/* exp used by the mixture density: libm by default; orc_set_map_exp()
+ * swaps in another implementation (the device's deterministic gq_exp from
+ * the emulator) so the MAP restatement can be compared bit for bit.  The
+ * reference's get_map_mex uses its own runtime's exp (parity unpinned). */
+static double (*map_exp)(double) = exp;
+void orc_set_map_exp(double (*f)(double)) { map_exp = f ? f : exp; }
+
 static double neg_mix(double x, const double *a, const double *u, const double *o, int L)
 {
     double v = 0;
     for (int l = 0; l < L; ++l) {
         const double z = (x - u[l]) / o[l];
-        v += a[l] * (exp(-0.5 * z * z) / (sqrt(2 * M_PI) * o[l]));
+        v += a[l] * (map_exp(-0.5 * z * z) / (sqrt(2 * M_PI) * o[l]));
     }
     return -v;
 }

@@ -113,6 +113,8 @@ typedef struct {
  * state on entry (mu = flow, sigma = rand + 2, rou = 0 in the reference) and
  * the result on exit; trace[3*i] = max|dmu|, max|dsigma|, max|drou| of
  * iteration i+1.  Returns the number of iterations run. */
+/* exp of the mixture density in orc_get_map (NULL: libm exp). */
+void orc_set_map_exp(double (*f)(double));
 int orc_cpu_run(const orc_cpu_params *P, const double *X, const double *W, const double *flow, int M, int N,
                 double *mu, double *sigma, double *rou, double *trace, int nthreads);
 

@@ -208,13 +208,22 @@ def aepe(tflow, flow, unknown, r0: int = 1) -> float:
     return f(_p(tflow), _p(flow), unk.ctypes.data_as(C.POINTER(C.c_ubyte)), M, N, r0)
 
 
-def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0) -> np.ndarray:
+def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0, det_exp: bool = False) -> np.ndarray:
+    """findMixMax.m:39-70 with MATLAB fminbnd.  det_exp: the mixture density
+    uses the device's deterministic exp (gqmap_math.h gq_exp) instead of
+    libm's, so the result is comparable bit for bit with k_mixture_map."""
     muu, sigu, muv, sigv = map(_f64, (muu, sigu, muv, sigv))
     alpha = _f64(np.ravel(alpha))
     M, N, L = muu.shape
     out = np.zeros((M, N, 2), order="F")
-    lib().orc_get_map(_p(alpha), _p(muu), _p(sigu), _p(muv), _p(sigv), M, N, L, _p(out),
-                      nthreads)
+    L_ = lib()
+    L_.orc_set_map_exp.argtypes = [C.c_void_p]
+    if det_exp:
+        L_.orc_set_map_exp(C.cast(L_.emu_gq_exp, C.c_void_p))
+    try:
+        L_.orc_get_map(_p(alpha), _p(muu), _p(sigu), _p(muv), _p(sigv), M, N, L, _p(out), nthreads)
+    finally:
+        L_.orc_set_map_exp(None)
     return out
 
 

@@ -149,3 +149,18 @@ def test_get_map_mixture_between_modes(oracle_lib):
     sg = np.ones((1, 1, 2))
     out = oracle_lib.get_map([0.5, 0.5], mu, sg, mu, sg)
     assert abs(out[0, 0, 0] - 0.25) < 1e-3
+
+
+def test_map_deterministic_exp_mode(oracle_lib):
+    """get_map with det_exp uses the device's gq_exp (within 1 ulp of libm):
+    maxima agree to the fminbnd tolerance on well-separated mixtures, and the
+    libm default is restored afterwards."""
+    rng = np.random.default_rng(3)
+    M, N, L = 12, 14, 2
+    mu = np.asfortranarray(np.stack([rng.normal(-4, 0.3, (M, N)), rng.normal(4, 0.3, (M, N))], axis=2))
+    sg = np.asfortranarray(rng.random((M, N, L)) * 0.5 + 0.2)
+    a = np.array([0.7, 0.3])
+    x = oracle_lib.get_map(a, mu, sg, mu, sg)
+    y = oracle_lib.get_map(a, mu, sg, mu, sg, det_exp=True)
+    np.testing.assert_allclose(x, y, atol=1e-4)
+    np.testing.assert_array_equal(oracle_lib.get_map(a, mu, sg, mu, sg), x)
