@@ -23,12 +23,12 @@ LMAX, KMAX = 8, 16
 # Every entry point declared in include/gqmap.h (checked by tests/test_abi.py).
 EXPORTS = (
     "gqmap_options_default", "gqmap_options_alpha_mode", "gqmap_create", "gqmap_set_images", "gqmap_init_state",
-    "gqmap_set_state", "gqmap_get_state", "gqmap_run", "gqmap_run_timed", "gqmap_get_info",
+    "gqmap_set_state", "gqmap_get_state", "gqmap_run", "gqmap_run_aepe", "gqmap_set_truth", "gqmap_run_timed", "gqmap_get_info",
     "gqmap_get_map", "gqmap_log_p", "gqmap_synchronize", "gqmap_destroy", "gqmap_projsplx",
     "gqmap_mixture_map", "gqmap_flow_to_color", "gqmap_gauss_hermite", "gqmap_rand_uniform",
     "gqmap_last_error", "gqmap_abi_version", "gqmap_device_count", "gqmap_imresize",
     "gqmap_warp_image", "gqmap_ctf_create", "gqmap_ctf_set_images", "gqmap_ctf_run",
-    "gqmap_ctf_get_level", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
+    "gqmap_ctf_get_level", "gqmap_ctf_set_truth", "gqmap_ctf_get_trace", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
     "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run",
     "gqmap_cpu_options_default", "gqmap_cpu_run", "gqmap_cpu_release", "gqmap_read_flo", "gqmap_write_flo", "gqmap_aepe",
 )
@@ -99,6 +99,8 @@ def load():
         "gqmap_set_state": (C.c_int, [vp, P(GqmapState)]),
         "gqmap_get_state": (C.c_int, [vp, P(GqmapState)]),
         "gqmap_run": (C.c_int, [vp, C.c_int, P(C.c_int), _D]),
+        "gqmap_run_aepe": (C.c_int, [vp, C.c_int, P(C.c_int), _D, _D]),
+        "gqmap_set_truth": (C.c_int, [vp, _D, C.c_int, C.c_int]),
         "gqmap_run_timed": (C.c_int, [vp, C.c_int, P(C.c_int), _D, _D]),
         "gqmap_get_info": (C.c_int, [vp, P(GqmapInfo)]),
         "gqmap_get_map": (C.c_int, [vp, _D]),
@@ -119,6 +121,8 @@ def load():
         "gqmap_ctf_set_images": (C.c_int, [vp, _D, _D, C.c_int, C.c_int]),
         "gqmap_ctf_run": (C.c_int, [vp, C.c_uint64, _D, P(C.c_int), _D]),
         "gqmap_ctf_get_level": (C.c_int, [vp, C.c_int, P(C.c_int), P(C.c_int), _D, _D, _D, _D]),
+        "gqmap_ctf_set_truth": (C.c_int, [vp, _D, C.c_int, C.c_int]),
+        "gqmap_ctf_get_trace": (C.c_int, [vp, C.c_int, P(C.c_int), _D, _D]),
         "gqmap_ctf_destroy": (None, [vp]),
         "gqmap_resize_len": (C.c_int, [C.c_int, C.c_double]),
         "gqmap_create_tile": (C.c_int, [P(vp), P(GqmapOptions), C.c_int, C.c_int, C.c_int]),

@@ -126,7 +126,8 @@ constexpr int TS = TAB_STRIDE;
 constexpr int NPLANES = 9;
 constexpr int TRACE_CAP = 8192;
 constexpr int GRAPH_CHUNK = 50;
-constexpr int NFIX = 4;        // fixed slots per block: Energy, sum|dmu_u|, sum|dsig_u|, #nonfinite
+constexpr int NFIX = 5;        // fixed slots per block: Energy, sum|dmu_u|, sum|dsig_u|, #nonfinite, AEPE sum
+constexpr int TRACE_W = 4;     // trace ring columns: Energy, ptdmu, ptdsigma, AEPE (NaN without a truth)
 
 struct Ctl {
     int it;    // next iteration (1-based)
@@ -151,7 +152,8 @@ struct FinParams {
     const fix128 *gathered;  // nranks > 0: per-tile totals [nranks][NFIX+L] (exact, any order)
     int nranks;
     Ctl *ctl;
-    double *trace;     // TRACE_CAP x 3
+    double *trace;     // TRACE_CAP x TRACE_W
+    int aepe;          // 1: tot[4] is the AEPE sum of gqmap_ctf.m:38 (a truth is set)
     double count;      // interior nodes * L
     double step0, step_decay;
     int alpha_mode, alpha_start;
@@ -185,6 +187,7 @@ struct IterParams {
     R epsn, lamd, lams;
     R minu, maxu, minv, maxv, sig_lo, sig_hi, corr, sig_step;
     R gh_xmax;  // max |Gauss-Hermite node| (node_unclamped)
+    const double *truth;  // ctf engine: M x N x 2 top-left block of GRDT, or null (gqmap_set_truth)
     double step0, step_decay;
     int guard;
     int64_t MNL;
@@ -338,9 +341,12 @@ __device__ void fin_apply(const FinParams &F, const double *tot)
         }
     }
     const int slot = (it - 1) % TRACE_CAP;
-    F.trace[3 * slot + 0] = energy;
-    F.trace[3 * slot + 1] = ptdmu;
-    F.trace[3 * slot + 2] = ptdsig;
+    F.trace[TRACE_W * slot + 0] = energy;
+    F.trace[TRACE_W * slot + 1] = ptdmu;
+    F.trace[TRACE_W * slot + 2] = ptdsig;
+    // gqmap_ctf.m:38: mean(mean(sqrt((GRDT-mu)^2...))) over the interior after
+    // the update -- equal-length columns, so the exact total / count
+    F.trace[TRACE_W * slot + 3] = F.aepe ? (bad ? nan : tot[4] / F.count) : nan;
     if (F.t_decay_every > 0 && it % F.t_decay_every == 0) ctl->T = fmax(ctl->T * F.drate, F.t_min);
     ctl->it = it + 1;
     ctl->done = ctl->done + 1;
@@ -494,7 +500,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     auto &in_left = lds.in_left;
     auto &red = lds.red;
 
-    fix128 fE = 0, fmu = 0, fsg = 0;
+    fix128 fE = 0, fmu = 0, fsg = 0, fae = 0;
     int nonfinite = 0;
     const int wave = tid >> 6, lane = tid & 63;
     // halo: 4*TM edges (top row and left column, u and v) x Q lanes, whole waves
@@ -604,8 +610,16 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][pix]) + in_left[0][1][pix];
             const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
-            put_state<PIPE, R>(&dst[i + MNL * 0], cl(mu_u + gmu_u * step, P.minu, P.maxu));
-            put_state<PIPE, R>(&dst[i + MNL * 1], cl(mu_v + gmu_v * step, P.minv, P.maxv));
+            const R nu = cl(mu_u + gmu_u * step, P.minu, P.maxu), nv = cl(mu_v + gmu_v * step, P.minv, P.maxv);
+            put_state<PIPE, R>(&dst[i + MNL * 0], nu);
+            put_state<PIPE, R>(&dst[i + MNL * 1], nv);
+            if constexpr (ENG == 2) {  // AEPE of gqmap_ctf.m:38 against the updated mean
+                if (P.truth) {
+                    const double du = P.truth[m + (int64_t)M * n] - (double)nu;
+                    const double dv = P.truth[m + (int64_t)M * n + MN] - (double)nv;
+                    fae += to_fix(gq_sqrt_dev(du * du + dv * dv));
+                }
+            }
             // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
             const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
             const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
@@ -633,11 +647,13 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     fmu = wave_sum_fix(fmu);
     fsg = wave_sum_fix(fsg);
     fix128 fnf = wave_sum_fix((fix128)nonfinite);
+    if (ENG == 2) fae = wave_sum_fix(fae);
     if (lane == 0) {
         red[0][wave] = fE;
         red[1][wave] = fmu;
         red[2][wave] = fsg;
         red[3][wave] = fnf;
+        red[4][wave] = fae;
     }
     __syncthreads();
     const int NP = NFIX + P.L;
@@ -1054,6 +1070,7 @@ struct gqmap_ctx {
     Ctl *d_ctl = nullptr;
     fix128 *d_partials = nullptr;
     double *d_trace = nullptr;
+    double *d_truth = nullptr;  // gqmap_set_truth: M x N x 2 (ctf engine)
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     int *d_done_it = nullptr;  // pipelined kernel: per-tile completed iteration
     bool have_images = false, have_state = false;
@@ -1167,6 +1184,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     double xmax = 0;
     for (int k = 0; k < c->K2; ++k) xmax = std::max(xmax, std::fabs(c->tab_host[tab_at(0, k)]));
     P.gh_xmax = R(xmax);
+    P.truth = c->d_truth;
     P.step0 = o.step0; P.step_decay = o.step_decay;
     P.guard = o.guard_a;
     P.MNL = c->MNL;
@@ -1187,6 +1205,7 @@ FinParams fin_params(const gqmap_ctx *c)
     F.L = c->L;
     F.ctl = c->d_ctl;
     F.trace = c->d_trace;
+    F.aepe = c->d_truth != nullptr;
     F.count = (double)(c->M - 2) * (double)(c->Ng - 2) * c->L;  // global interior
     F.gathered = c->d_gathered;
     F.nranks = c->nranks;
@@ -1732,7 +1751,7 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
     }
     if (hipMalloc(&c->d_tab, NTAB * TS * c->rsz) != hipSuccess ||
         hipMalloc((void **)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
-        hipMalloc((void **)&c->d_trace, sizeof(double) * 3 * TRACE_CAP) != hipSuccess) {
+        hipMalloc((void **)&c->d_trace, sizeof(double) * TRACE_W * TRACE_CAP) != hipSuccess) {
         set_error("device allocation failed");
         return fail(GQMAP_ERR_OUT_OF_MEMORY);
     }
@@ -1871,21 +1890,59 @@ gqmap_status gqmap_get_state(gqmap_ctx *c, gqmap_state *st)
     return GQMAP_OK;
 }
 
-static gqmap_status fetch_trace(gqmap_ctx *c, int it_before, int n, double *trace)
+static gqmap_status fetch_trace(gqmap_ctx *c, int it_before, int n, double *trace, double *aepe = nullptr)
 {
-    if (!trace || n <= 0) return GQMAP_OK;
-    std::vector<double> ring((size_t)3 * TRACE_CAP);
+    if ((!trace && !aepe) || n <= 0) return GQMAP_OK;
+    std::vector<double> ring((size_t)TRACE_W * TRACE_CAP);
     GQ_HIP(hipMemcpyAsync(ring.data(), c->d_trace, ring.size() * sizeof(double),
                           hipMemcpyDeviceToHost, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     for (int i = 0; i < n; ++i) {
         const int slot = (it_before + i - 1) % TRACE_CAP;
-        for (int q = 0; q < 3; ++q) trace[3 * i + q] = ring[3 * slot + q];
+        if (trace)
+            for (int q = 0; q < 3; ++q) trace[3 * i + q] = ring[TRACE_W * slot + q];
+        if (aepe) aepe[i] = ring[TRACE_W * slot + 3];
     }
     return GQMAP_OK;
 }
 
 gqmap_status gqmap_run(gqmap_ctx *c, int n_iter, int *n_done, double *trace)
+{
+    return gqmap_run_aepe(c, n_iter, n_done, trace, nullptr);
+}
+
+gqmap_status gqmap_set_truth(gqmap_ctx *c, const double *grdt, int Mg, int Ng)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "gqmap_set_truth before gqmap_set_images");
+    GQ_CHECK(c->opt.engine == GQMAP_ENGINE_CTF, GQMAP_ERR_UNSUPPORTED,
+             "per-iteration AEPE is the ctf level engine's (legacy/gqmap_ctf.m:38)");
+    GQ_CHECK(c->n_tiles == 1, GQMAP_ERR_UNSUPPORTED, "gqmap_set_truth on a column-strip tile");
+    DeviceGuard dg(c->device);
+    drop_graph(c);  // the captured launches hold the previous truth pointer
+    if (!grdt) {
+        if (c->d_truth) GQ_HIP(hipFree(c->d_truth));
+        c->d_truth = nullptr;
+        return GQMAP_OK;
+    }
+    GQ_CHECK(Mg >= c->M && Ng >= c->N, GQMAP_ERR_INVALID_ARG, "truth %dx%d smaller than the grid %dx%d", Mg, Ng,
+             c->M, c->N);
+    // GRDT(M_,N_,:) of the array passed in: its top-left M x N block (the
+    // reference passes the full-resolution trueFlow.*scale to every level)
+    const size_t MN = (size_t)c->M * c->N;
+    std::vector<double> blk(2 * MN);
+    for (int k = 0; k < 2; ++k)
+        for (int n = 0; n < c->N; ++n)
+            std::memcpy(&blk[MN * k + (size_t)c->M * n], grdt + (size_t)Mg * Ng * k + (size_t)Mg * n,
+                        sizeof(double) * c->M);
+    if (!c->d_truth) GQ_HIP(hipMalloc((void **)&c->d_truth, sizeof(double) * 2 * MN));
+    GQ_HIP(hipMemcpyAsync(c->d_truth, blk.data(), sizeof(double) * 2 * MN, hipMemcpyHostToDevice, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace, double *aepe)
 {
     clear_error();
     GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
@@ -1919,7 +1976,8 @@ gqmap_status gqmap_run(gqmap_ctx *c, int n_iter, int *n_done, double *trace)
         Ctl h;
         if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
         const int ran = h.it - (h0.it + total);
-        if ((s = fetch_trace(c, h0.it + total, ran, trace ? trace + 3 * total : nullptr)) != GQMAP_OK)
+        if ((s = fetch_trace(c, h0.it + total, ran, trace ? trace + 3 * total : nullptr,
+                             aepe ? aepe + total : nullptr)) != GQMAP_OK)
             return s;
         total += ran;
         if (h.stop || ran < chunk) break;
@@ -2257,7 +2315,7 @@ void gqmap_destroy(gqmap_ctx *c)
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace,
-                    (void *)c->d_done_it};
+                    (void *)c->d_done_it, c->d_truth};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

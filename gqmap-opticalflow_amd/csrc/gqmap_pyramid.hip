@@ -282,6 +282,8 @@ struct gqmap_pyramid {
         Resampler img, pro;  // full-res -> level (frames); previous warp -> level (x2)
         gqmap_ctx *ctx = nullptr;
         int its_done = 0;
+        std::vector<double> energy, aepe;  // per iteration of the last run (gqmap_ctf's Energy, AEPE)
+        bool has_truth = false;
     };
     gqmap_options opt;
     int device = 0, nlev = 0;
@@ -295,6 +297,7 @@ struct gqmap_pyramid {
     int *flag = nullptr;
     Level lev[GQMAP_CTF_MAX_LEVELS];
     bool ran = false;
+    std::vector<double> truth;  // gqmap_ctf_set_truth: full-resolution trueFlow, M x N x 2 (host)
 
     void release_levels()
     {
@@ -479,6 +482,7 @@ gqmap_status gqmap_ctf_set_images(gqmap_pyramid *p, const double *img1, const do
         o.minv *= L.scale;
         o.maxv *= L.scale;
         s = gqmap_create(&L.ctx, &o, p->device);
+        L.has_truth = false;
         if (s != GQMAP_OK) return s;
         ctx_adopt_stream(L.ctx, p->stream);
     }
@@ -504,9 +508,29 @@ gqmap_status gqmap_ctf_run(gqmap_pyramid *p, uint64_t seed, double *flow, int *i
         gqmap_status s = ctx_set_images_device(L.ctx, L.I1w, L.I2, L.M, L.N, p->vv, p->flag);
         if (s != GQMAP_OK) return s;
         if ((s = gqmap_init_state(L.ctx, seed + (uint64_t)l)) != GQMAP_OK) return s;
+        // gqmap_ctf(options,I1_w,I2,trueFlow.*scale) (:33): GRDT is the full
+        // resolution GT times the level scale; the level reads its top-left block
+        if (!p->truth.empty()) {
+            const size_t MN = (size_t)p->M * p->N;
+            std::vector<double> blk(2 * (size_t)L.M * L.N);
+            for (int k = 0; k < 2; ++k)
+                for (int n = 0; n < L.N; ++n)
+                    for (int m = 0; m < L.M; ++m)
+                        blk[(size_t)L.M * L.N * k + (size_t)L.M * n + m] = p->truth[MN * k + (size_t)p->M * n + m] * L.scale;
+            if ((s = gqmap_set_truth(L.ctx, blk.data(), L.M, L.N)) != GQMAP_OK) return s;
+            L.has_truth = true;
+        } else if (L.has_truth) {
+            if ((s = gqmap_set_truth(L.ctx, nullptr, 0, 0)) != GQMAP_OK) return s;
+            L.has_truth = false;
+        }
         int done = 0;
-        if ((s = gqmap_run(L.ctx, p->opt.its, &done, nullptr)) != GQMAP_OK) return s;
+        std::vector<double> tr(3 * (size_t)std::max(p->opt.its, 1));
+        L.aepe.assign((size_t)std::max(p->opt.its, 1), 0.0);
+        if ((s = gqmap_run_aepe(L.ctx, p->opt.its, &done, tr.data(), L.aepe.data())) != GQMAP_OK) return s;
         L.its_done = done;
+        L.aepe.resize(done);
+        L.energy.resize(done);
+        for (int i = 0; i < done; ++i) L.energy[i] = tr[3 * (size_t)i];
         const void *muu, *muv;
         bool f32;
         if ((s = ctx_flow_device(L.ctx, &muu, &muv, &f32)) != GQMAP_OK) return s;
@@ -548,6 +572,33 @@ gqmap_status gqmap_ctf_get_level(gqmap_pyramid *p, int level, int *Ml, int *Nl, 
     if ((s = download_d(I2, L.I2, mn, p->stream)) != GQMAP_OK) return s;
     if ((s = download_d(flow, L.flow, 2 * mn, p->stream)) != GQMAP_OK) return s;
     return download_d(warp, L.warp, 2 * mn, p->stream);
+}
+
+gqmap_status gqmap_ctf_set_truth(gqmap_pyramid *p, const double *flow, int M, int N)
+{
+    clear_error();
+    GQ_CHECK(p, GQMAP_ERR_INVALID_ARG, "null pyramid");
+    if (!flow) {
+        p->truth.clear();
+        return GQMAP_OK;
+    }
+    GQ_CHECK(p->lev[0].ctx, GQMAP_ERR_STATE, "gqmap_ctf_set_truth before gqmap_ctf_set_images");
+    GQ_CHECK(M == p->M && N == p->N, GQMAP_ERR_INVALID_ARG, "truth %dx%d, frames %dx%d", M, N, p->M, p->N);
+    p->truth.assign(flow, flow + 2 * (size_t)M * N);
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_ctf_get_trace(gqmap_pyramid *p, int level, int *n, double *energy, double *aepe)
+{
+    clear_error();
+    GQ_CHECK(p, GQMAP_ERR_INVALID_ARG, "null pyramid");
+    GQ_CHECK(level >= 0 && level < p->nlev, GQMAP_ERR_INVALID_ARG, "level %d of %d", level, p->nlev);
+    GQ_CHECK(p->ran, GQMAP_ERR_STATE, "gqmap_ctf_get_trace before gqmap_ctf_run");
+    const gqmap_pyramid::Level &L = p->lev[level];
+    if (n) *n = L.its_done;
+    if (energy) std::copy(L.energy.begin(), L.energy.end(), energy);
+    if (aepe) std::copy(L.aepe.begin(), L.aepe.end(), aepe);
+    return GQMAP_OK;
 }
 
 void gqmap_ctf_destroy(gqmap_pyramid *p)

@@ -173,6 +173,28 @@ class Engine:
         check(self.lib.gqmap_run(self.ctx, int(n_iter), C.byref(done), dptr(trace)), "gqmap_run")
         return done.value, trace[:done.value]
 
+    def set_truth(self, grdt) -> None:
+        """Ground truth of the ctf level engine (gqmap_set_truth): GRDT of
+        gqmap_ctf(options,I1,I2,GRDT), Mg x Ng x 2 with Mg >= M, Ng >= N (its
+        top-left M x N block is used, as gqmap_ctf.m:38 does); None clears."""
+        if grdt is None:
+            check(self.lib.gqmap_set_truth(self.ctx, None, 0, 0), "gqmap_set_truth")
+            return
+        g = f64(grdt)
+        if g.ndim != 3 or g.shape[2] != 2:
+            raise ValueError("truth must be Mg x Ng x 2")
+        check(self.lib.gqmap_set_truth(self.ctx, dptr(g), g.shape[0], g.shape[1]), "gqmap_set_truth")
+
+    def run_aepe(self, n_iter: int):
+        """run() plus the per-iteration AEPE of gqmap_ctf.m:38 (NaN without a
+        truth): (n_done, trace[n_done, 3], aepe[n_done])."""
+        trace = np.zeros((max(n_iter, 1), 3))
+        ae = np.zeros(max(n_iter, 1))
+        done = C.c_int(0)
+        check(self.lib.gqmap_run_aepe(self.ctx, int(n_iter), C.byref(done), dptr(trace), dptr(ae)),
+              "gqmap_run_aepe")
+        return done.value, trace[:done.value], ae[:done.value]
+
     def run_timed(self, n_iter: int):
         done, tot, ker = C.c_int(0), C.c_double(0), C.c_double(0)
         check(self.lib.gqmap_run_timed(self.ctx, int(n_iter), C.byref(done), C.byref(tot),

@@ -34,37 +34,28 @@ def ctf_options(options: dict | None = None, **kw) -> dict:
 
 
 def gqmap_ctf(options: dict, I1, I2, GRDT, *, seed: int = 0, precision: str = "fp64",
-              device: int = 0, eval_every: int = 200):
+              device: int = 0):
     """[mu, sigma, rou, AEPE, Energy] = gqmap_ctf(options, I1, I2, GRDT).
 
-    minu..maxv come from GRDT (gqmap_ctf.m:4).  AEPE is evaluated against
-    GRDT(M_,N_,:) at it == 1 and every `eval_every` iterations (the reference
-    evaluates it every iteration; NaN elsewhere here)."""
+    minu..maxv come from GRDT (gqmap_ctf.m:4).  AEPE(it) is the reference's
+    per-iteration mean(mean(sqrt((GRDT(M_,N_,1)-muu(M_,N_)).^2 + ...)))
+    (gqmap_ctf.m:38), reduced exactly on the device inside the iteration
+    kernel (GRDT may be larger than I1: its top-left block is used, as the
+    reference indexes it).  Iterations after a stop keep the reference's
+    initial value 17 (AEPE = ones(its,1)*17, :13); Energy after a stop is 0."""
     GRDT = f64(GRDT)
     o = dict(options)
     o.update(minu=float(GRDT[:, :, 0].min()), maxu=float(GRDT[:, :, 0].max()),
              minv=float(GRDT[:, :, 1].min()), maxv=float(GRDT[:, :, 1].max()))
     its = int(o["its"])
-    AEPE = np.full(its, np.nan)
+    AEPE = np.full(its, 17.0)
     Energy = np.zeros(its)
     with Engine(o, I1, I2, "ctf", precision, device) as eng:
         eng.init_state(seed)
-        M, N = eng.M, eng.N
-        it = 1
-        while it <= its:
-            nxt = 1 if it == 1 else min(its, (it // eval_every + 1) * eval_every)
-            n = nxt - it + 1
-            done, tr = eng.run(n)
-            Energy[it - 1: it - 1 + done] = tr[:, 0]
-            last = it + done - 1
-            if done:
-                st = eng.get_state()
-                # gqmap_ctf.m:38 -- GRDT(M_,N_) of the array passed in
-                d = GRDT[1:M - 1, 1:N - 1] - np.stack([st.muu[1:-1, 1:-1, 0], st.muv[1:-1, 1:-1, 0]], 2)
-                AEPE[last - 1] = float(np.mean(np.mean(np.sqrt(np.sum(d ** 2, axis=2)), axis=0)))
-            it += done
-            if done < n:
-                break
+        eng.set_truth(GRDT)
+        done, tr, ae = eng.run_aepe(its)
+        Energy[:done] = tr[:, 0]
+        AEPE[:done] = ae
         st = eng.get_state()
     mu = np.stack([st.muu[:, :, 0], st.muv[:, :, 0]], axis=2)
     sigma = np.stack([st.sigu[:, :, 0], st.sigv[:, :, 0]], axis=2)
@@ -91,6 +82,24 @@ class Pyramid:
         self.M, self.N = img1.shape
         check(self.lib.gqmap_ctf_set_images(self.ptr, dptr(img1), dptr(img2), self.M, self.N),
               "gqmap_ctf_set_images")
+
+    def set_truth(self, true_flow) -> None:
+        """Full-resolution trueFlow (M x N x 2, as flowToColor returns it):
+        each level then records gqmap_ctf's per-iteration AEPE against
+        trueFlow.*scale (optical_flow_ctf.m:33).  None clears it."""
+        if true_flow is None:
+            check(self.lib.gqmap_ctf_set_truth(self.ptr, None, 0, 0), "gqmap_ctf_set_truth")
+            return
+        t = f64(true_flow)
+        check(self.lib.gqmap_ctf_set_truth(self.ptr, dptr(t), t.shape[0], t.shape[1]), "gqmap_ctf_set_truth")
+
+    def trace(self, l: int):
+        """Level l of the last run: (Energy, AEPE) per iteration (gqmap_ctf's outputs)."""
+        n = C.c_int(0)
+        check(self.lib.gqmap_ctf_get_trace(self.ptr, l, C.byref(n), None, None), "gqmap_ctf_get_trace")
+        e, a = np.zeros(max(n.value, 1)), np.zeros(max(n.value, 1))
+        check(self.lib.gqmap_ctf_get_trace(self.ptr, l, None, dptr(e), dptr(a)), "gqmap_ctf_get_trace")
+        return e[:n.value], a[:n.value]
 
     def run(self, seed: int = 0):
         """Returns (flow M x N x 2, iterations per level, wall ms)."""

@@ -138,6 +138,14 @@ gqmap_status gqmap_run(gqmap_ctx *ctx, int n_iter, int *n_done, double *trace);
 /* Same as gqmap_run with n_iter iterations, timed on the context's stream
  * with HIP events: total_ms over all launches, iter_kernel_ms = sum of the
  * fused iteration kernel's durations (event pair around each launch). */
+/* Ground truth of the ctf level engine: GRDT Mg x Ng x 2 (Mg >= M, Ng >= N;
+ * its top-left M x N block is used, as gqmap_ctf.m:38 indexes GRDT(M_,N_,:)
+ * of whatever it is passed).  NULL clears it.  With a truth set every
+ * iteration also reduces the AEPE of the updated mean on the device. */
+gqmap_status gqmap_set_truth(gqmap_ctx *ctx, const double *grdt, int Mg, int Ng);
+/* gqmap_run plus aepe[n_done] (optional): the per-iteration AEPE of
+ * gqmap_ctf.m:38 (NaN when no truth is set) -- the reference's AEPE output. */
+gqmap_status gqmap_run_aepe(gqmap_ctx *ctx, int n_iter, int *n_done, double *trace, double *aepe);
 gqmap_status gqmap_run_timed(gqmap_ctx *ctx, int n_iter, int *n_done, double *total_ms,
                              double *iter_kernel_ms);
 gqmap_status gqmap_get_info(gqmap_ctx *ctx, gqmap_info *info);
@@ -226,6 +234,13 @@ gqmap_status gqmap_ctf_run(gqmap_pyramid *p, uint64_t seed, double *flow, int *i
  * the level (Ml x Nl x 2). */
 gqmap_status gqmap_ctf_get_level(gqmap_pyramid *p, int level, int *Ml, int *Nl, double *I1w,
                                  double *I2, double *flow, double *warp);
+/* trueFlow (M x N x 2, the full-resolution GT as flowToColor returns it):
+ * every level then records gqmap_ctf's per-iteration AEPE against
+ * trueFlow.*scale (optical_flow_ctf.m:33, gqmap_ctf.m:38).  NULL clears it. */
+gqmap_status gqmap_ctf_set_truth(gqmap_pyramid *p, const double *flow, int M, int N);
+/* Per-iteration Energy and AEPE (NaN without a truth) of level `level` in the
+ * last gqmap_ctf_run; *n = its_done of the level (each array may be NULL). */
+gqmap_status gqmap_ctf_get_trace(gqmap_pyramid *p, int level, int *n, double *energy, double *aepe);
 void gqmap_ctf_destroy(gqmap_pyramid *p);
 
 /* ---- legacy flow-denoising engine: legacy/gqmap_cpu.m ----

@@ -91,3 +91,17 @@ def test_options_defaults_mirror_reference():
     assert (s.K, s.lambdas, s.step0, s.step_decay, s.sig_hi, s.guard_a, s.t_decay_every) == \
         (11, 16.0, 0.001, 4000.0, 25.0, 0, 500)
     assert o.corr_tor == 1 - 1e-5 and o.tor == 1e-4 and o.alpha_start == 500 and o.alpha_lr == 1e-7
+
+
+def test_mex_gateways_build_and_reject_bad_calls_without_a_device():
+    """The MEX gateways compile against the MEX API shim and check their
+    argument lists before touching the device (gqmap:usage)."""
+    import pytest
+    from tests._mexshim import Gateway, build
+    try:
+        build()
+    except Exception as e:  # no libgqmap.so in this environment
+        pytest.skip(f"MEX shim build: {e}")
+    for name in ("mixture", "super", "ctf"):
+        with pytest.raises(RuntimeError, match="usage"):
+            Gateway(name)(1, dict(its=1))

@@ -111,8 +111,10 @@ def test_gqmap_ctf_single_level_and_driver():
     mu, sigma, rou, AEPE, Energy = gqmap_ctf(dict(K=11, its=40, epsn=1e-6, lambdas=5, lambdad=1),
                                              I1, I2, flo)
     assert mu.shape == (64, 96, 2) and rou.shape == (64, 96, 2, 2)
-    assert np.isfinite(AEPE[0]) and np.isfinite(AEPE[-1]) and np.isnan(AEPE[5])
-    assert (Energy != 0).all()
+    assert np.isfinite(AEPE).all() and (Energy != 0).all()
+    # the last AEPE is gqmap_ctf.m:38 on the returned mean
+    d = flo[1:-1, 1:-1] - mu[1:-1, 1:-1]
+    assert AEPE[-1] == pytest.approx(np.mean(np.mean(np.sqrt(np.sum(d ** 2, axis=2)), axis=0)), rel=1e-12)
     flow, a, its, ms = optical_flow_ctf(I1, I2, flo, dict(its=20), scales=(0.25, 0.5, 1.0))
     assert flow.shape == (64, 96, 2) and np.isfinite(a) and len(its) == 3
 
@@ -126,3 +128,53 @@ def test_pyramid_rejects_inconsistent_geometry():
             p.set_images(I1, I1)
     with pytest.raises(GqmapError, match="scale 1"):
         Pyramid(ctf_options(minu=-1, maxu=1, minv=-1, maxv=1), (0.25, 0.5))
+
+
+def test_ctf_aepe_every_iteration_matches_host():
+    """gqmap_ctf.m:38 records AEPE every iteration: the device reduction
+    (exact fixed-point sum inside the iteration kernel) equals the host mean
+    of means on the state after each iteration; a GRDT larger than the level
+    contributes its top-left block, as the reference indexes it."""
+    from gqmap_opticalflow_amd import Engine
+    I1, I2, flo, unk, rng = _pipeline_pair("Grove3", (100, 100, 64, 96))
+    big = np.asfortranarray(np.pad(flo, ((0, 7), (0, 5), (0, 0)), constant_values=3.0) * 0.5)
+    o = dict(K=11, its=30, epsn=1e-6, lambdas=5, lambdad=1, minu=-2, maxu=2, minv=-2, maxv=2)
+    with Engine(o, I1, I2, "ctf") as a, Engine(o, I1, I2, "ctf") as b:
+        a.init_state(4)
+        b.init_state(4)
+        a.set_truth(big)
+        done, tr, ae = a.run_aepe(12)
+        assert done == 12
+        g = big[:64, :96]
+        for k in range(12):
+            _, trb = b.run(1)
+            np.testing.assert_array_equal(trb[0], tr[k])  # the truth does not perturb the solve
+            st = b.get_state()
+            d = g[1:-1, 1:-1] - np.stack([st.muu[1:-1, 1:-1, 0], st.muv[1:-1, 1:-1, 0]], axis=2)
+            ref = np.mean(np.mean(np.sqrt(np.sum(d ** 2, axis=2)), axis=0))
+            assert ae[k] == pytest.approx(ref, rel=1e-12, abs=0)
+        a.set_truth(None)
+        _, _, ae2 = a.run_aepe(2)
+        assert np.isnan(ae2).all()
+
+
+def test_pyramid_level_aepe_traces():
+    """optical_flow_ctf.m:33: each level's gqmap_ctf gets trueFlow.*scale;
+    its per-iteration AEPE (gqmap_ctf.m:38) is kept per level."""
+    from gqmap_opticalflow_amd import Pyramid, ctf_options
+    I1, I2, flo, unk, rng = _pipeline_pair("Grove3", (100, 100, 64, 96))
+    scales = (0.25, 0.5, 1.0)
+    with Pyramid(ctf_options(its=15, **rng), scales) as p:
+        p.set_images(I1, I2)
+        p.set_truth(flo)
+        flow, its, ms = p.run(seed=2)
+        for l, s in enumerate(scales):
+            e, a = p.trace(l)
+            assert len(a) == its[l] and np.isfinite(a).all() and (e != 0).all()
+            lev = p.level(l)
+            m, n = lev["flow"].shape[:2]
+            d = (flo[:m, :n] * s)[1:-1, 1:-1] - lev["flow"][1:-1, 1:-1]
+            assert a[-1] == pytest.approx(np.mean(np.mean(np.sqrt(np.sum(d ** 2, axis=2)), axis=0)), rel=1e-12)
+        p.set_truth(None)
+        p.run(seed=2)
+        assert np.isnan(p.trace(0)[1]).all()
