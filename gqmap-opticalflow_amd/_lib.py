@@ -29,7 +29,8 @@ EXPORTS = (
     "gqmap_last_error", "gqmap_abi_version", "gqmap_device_count", "gqmap_imresize",
     "gqmap_warp_image", "gqmap_ctf_create", "gqmap_ctf_set_images", "gqmap_ctf_run",
     "gqmap_ctf_get_level", "gqmap_ctf_set_truth", "gqmap_ctf_get_trace", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
-    "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run",
+    "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run", "gqmap_tile_attach_host",
+    "gqmap_tile_exchange_sizes", "gqmap_tile_exchange_begin", "gqmap_tile_exchange_end",
     "gqmap_cpu_options_default", "gqmap_cpu_run", "gqmap_cpu_release", "gqmap_read_flo", "gqmap_write_flo", "gqmap_aepe",
 )
 CTF_MAX_LEVELS = 8
@@ -129,6 +130,10 @@ def load():
         "gqmap_comm_unique_id": (C.c_int, [u8]),
         "gqmap_tile_attach_rccl": (C.c_int, [vp, u8]),
         "gqmap_tile_group_run": (C.c_int, [P(vp), C.c_int, C.c_int, P(C.c_int), _D]),
+        "gqmap_tile_attach_host": (C.c_int, [vp]),
+        "gqmap_tile_exchange_sizes": (C.c_int, [vp, P(C.c_size_t)]),
+        "gqmap_tile_exchange_begin": (C.c_int, [vp, vp, vp, vp]),
+        "gqmap_tile_exchange_end": (C.c_int, [vp, vp, vp, vp, _D]),
         "gqmap_cpu_options_default": (None, [P(GqmapCpuOptions)]),
         "gqmap_cpu_release": (C.c_int, []),
         "gqmap_read_flo": (C.c_int, [C.c_char_p, P(C.c_int), P(C.c_int), _D]),

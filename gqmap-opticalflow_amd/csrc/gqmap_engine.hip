@@ -178,6 +178,11 @@ struct IterParams {
     // context has n_off = 0, [0, N), Ng = N.
     int n_off, own_lo, own_hi, Ng;
     int tiles_m, tiles_n;
+    // the tiles of this launch: up to two runs of column-major tile indices
+    // [seg_lo[s], seg_lo[s] + seg_n[s]) (a tile context launches its boundary
+    // tile columns and its interior separately, to overlap the ghost-column
+    // exchange); block b writes partial row part_off + b
+    int seg_lo[2], seg_n[2], part_off;
     // fused finalize: the last workgroup to finish (arrival ticket in Ctl)
     // reduces the partials and runs the k_finalize step in the same launch
     int fused;
@@ -683,22 +688,24 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
 #if GQ_TIMELINE
     const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int nb = P.tiles_m * P.tiles_n;
+    const int nb = P.seg_n[0] + P.seg_n[1];  // tiles in this launch
     const int b = blockIdx.x;
     // lpar > 1: one block per (tile, component), component-major
     const int bt = P.lpar > 1 ? b % nb : b;
     const int l0 = P.lpar > 1 ? b / nb : 0, l1 = P.lpar > 1 ? l0 + 1 : P.L;
-    const int tile = tile_of_block(bt, nb, P.cu_group, P.cu_slots);
+    const int tl = tile_of_block(bt, nb, P.cu_group, P.cu_slots);
+    const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
     // workgroups that start on one CU are local blocks j, j+S, j+2S of the
     // XCD (see tile_of_block): alternate the phase order among them.  Not
     // for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
     const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
     const int NP = NFIX + P.L;
     __shared__ TileLds<R, BLOCK / Q> lds;
+    fix128 *part_row = P.partials + (int64_t)(P.part_off + b) * NP;
     if (edge_first)
-        iter_tile<R, VT, ENG, Q, false, true>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, false, true>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
     else
-        iter_tile<R, VT, ENG, Q, false, false>(P, tile, ctl->it, ctl->done & 1, P.partials + (int64_t)b * NP, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, false, false>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
 #if GQ_TIMELINE
     __syncthreads();
     if (threadIdx.x == 0 && ctl->it == GQ_TIMELINE && b < 8192) {
@@ -944,19 +951,30 @@ __global__ __launch_bounds__(256) void k_reduce_local(const fix128 *partials, in
 
 // Ghost-column exchange: the column k_iter just wrote (the ping-pong
 // destination, chosen by the device-side parity) <-> a contiguous buffer of
-// NPLANES x L x M values.  Column-major planes make each (plane, component)
-// column one contiguous run of M.
+// np x L x M values, the planes listed 4 bits each in `planes`.  Column-major
+// planes make each (plane, component) column one contiguous run of M.
+//
+// Only what the neighbour reads travels.  A tile recomputes the edges between
+// its left ghost and its first owned column -- they are the ghost's right
+// edges (dir 2): u1, o1 and rou(dir 2) of the ghost, gqmap_gpu_mixture.m:31-35
+// -- and its last owned column's right edges into the right ghost read that
+// ghost's mu and sigma.  pn and rou(dir 1) of a ghost are never read.
+constexpr uint32_t HALO_TO_LEFT = 0x3210;      // mu_u, mu_v, sigma_u, sigma_v
+constexpr int HALO_TO_LEFT_N = 4;
+constexpr uint32_t HALO_TO_RIGHT = 0x863210;   // + rou(dir 2, u), rou(dir 2, v) (planes 6, 8)
+constexpr int HALO_TO_RIGHT_N = 6;
+
 template <typename R>
 __global__ void k_halo_copy(const Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL, int L, int col,
-                            R *buf, int to_buf)
+                            uint32_t planes, int np, R *buf, int to_buf)
 {
     if (ctl->stop) return;
     R *dst = (ctl->done & 1) ? st0 : st1;
-    const int64_t n = (int64_t)NPLANES * L * M;
+    const int64_t n = (int64_t)np * L * M;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
         const int m = (int)(t % M);
-        const int64_t ql = t / M;  // q * L + l
-        const int q = (int)(ql / L), l = (int)(ql % L);
+        const int64_t ql = t / M;  // qi * L + l
+        const int q = (int)((planes >> (4 * (int)(ql / L))) & 15u), l = (int)(ql % L);
         R *p = dst + (int64_t)q * MNL + (int64_t)l * MN + (int64_t)col * M + m;
         if (to_buf) buf[t] = *p;
         else *p = buf[t];
@@ -1089,9 +1107,16 @@ struct gqmap_ctx {
     int nranks = 0;
     fix128 *d_gathered = nullptr;
     bool own_gathered = false;
+    // d_halo: send left (HALO_TO_LEFT planes), send right (HALO_TO_RIGHT),
+    // receive left (the left neighbour's send right), receive right
     void *d_halo[4] = {nullptr, nullptr, nullptr, nullptr};
     struct RcclComm *comm = nullptr;
     bool in_group = false;
+    bool host_xfer = false;  // gqmap_tile_attach_host: the caller moves the data
+    // RCCL tiles: the ghost-column exchange runs on `side` while the interior
+    // tiles run on `stream` (fork / join events)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_bnd = nullptr, ev_inr = nullptr, ev_xch = nullptr;
 };
 
 namespace {
@@ -1126,6 +1151,14 @@ int choose_lpar(const gqmap_ctx *c)
     static const char *e = std::getenv("GQMAP_LPAR");
     if (e && *e == '1') return 1;
     return c->super_ && c->L > 1 ? c->L : 1;
+}
+
+// Bytes of ghost-column buffer k (send left, send right, receive left,
+// receive right): a column of M values per (plane, component).
+size_t halo_bytes(const gqmap_ctx *c, int k)
+{
+    const int np = (k == 0 || k == 3) ? HALO_TO_LEFT_N : HALO_TO_RIGHT_N;
+    return (size_t)np * c->L * c->M * c->rsz;
 }
 
 gqmap_status alloc_grid(gqmap_ctx *c)
@@ -1177,6 +1210,10 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.M = c->M; P.N = c->N; P.Mo = c->Mo; P.No = c->No; P.M2 = c->Mo + 2;
     P.L = c->L; P.K2 = c->K2;
     P.tiles_m = c->tiles_m; P.tiles_n = c->tiles_n;
+    P.seg_lo[0] = P.seg_lo[1] = 0;
+    P.seg_n[0] = c->tiles_m * c->tiles_n;
+    P.seg_n[1] = 0;
+    P.part_off = 0;
     P.epsn = R(o.epsn); P.lamd = R(o.lambdad); P.lams = R(o.lambdas);
     P.minu = R(o.minu); P.maxu = R(o.maxu); P.minv = R(o.minv); P.maxv = R(o.maxv);
     P.sig_lo = R(o.sig_lo); P.sig_hi = R(o.sig_hi); P.corr = R(o.corr_tor);
@@ -1228,10 +1265,44 @@ int2 kernel_shape(K kern)
     return make_int2(std::max(1, per_cu), std::max(8, cus));
 }
 
+// A subset of the tiles for one k_iter launch (tile contexts: boundary tile
+// columns / interior), see IterParams::seg_lo.
+struct TileSegs {
+    int lo[2], n[2];
+    int part_off;
+};
+
+// The boundary tile columns of a column-strip tile (those holding its first
+// and last owned node columns: their results are what the neighbours need)
+// and the rest.  Together they cover every tile once; block partial rows
+// [0, bnd) and [bnd, nblocks).
+void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
+{
+    const int TM = c->split == 1 ? 16 : c->split == 4 ? 8 : 4;
+    const int tm = c->tiles_m, cb0 = c->own_lo / TM, cb1 = (c->own_hi - 1) / TM;
+    bnd.lo[0] = cb0 * tm; bnd.n[0] = tm;
+    bnd.lo[1] = cb1 * tm; bnd.n[1] = cb1 != cb0 ? tm : 0;
+    bnd.part_off = 0;
+    inr.lo[0] = (cb0 + 1) * tm; inr.n[0] = std::max(0, cb1 - cb0 - 1) * tm;
+    inr.lo[1] = (cb1 + 1) * tm; inr.n[1] = (c->tiles_n - cb1 - 1) * tm;
+    inr.part_off = (bnd.n[0] + bnd.n[1]) * c->lpar;
+    // columns before cb0 would be ghosts only (own_lo <= 1 < TM): none
+}
+
 template <typename R, typename VT, int ENG, int Q>
-void launch_k_iter(gqmap_ctx *c, int pipe_n)
+void launch_k_iter(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
 {
     IterParams<R, VT> P = iter_params<R, VT>(c);
+    int nblocks = c->nblocks;
+    if (sg) {
+        for (int k = 0; k < 2; ++k) {
+            P.seg_lo[k] = sg->lo[k];
+            P.seg_n[k] = sg->n[k];
+        }
+        P.part_off = sg->part_off;
+        nblocks = (sg->n[0] + sg->n[1]) * c->lpar;
+        if (nblocks == 0) return;
+    }
     if (pipe_n > 0) {
         static const int2 shp = kernel_shape(k_iter_pipe<R, VT, ENG, Q>);
         const int nb = c->nblocks;
@@ -1248,36 +1319,37 @@ void launch_k_iter(gqmap_ctx *c, int pipe_n)
         if (const char *g = getenv("GQMAP_CU_GROUP")) P.cu_group = atoi(g);
         if (getenv("GQMAP_CU_GROUP_PRINT")) fprintf(stderr, "k_iter Q=%d cu_group %d cu_slots %d\n", Q, P.cu_group, P.cu_slots);
     }
-    k_iter<R, VT, ENG, Q><<<c->nblocks, BLOCK, 0, c->stream>>>(P);
+    k_iter<R, VT, ENG, Q><<<nblocks, BLOCK, 0, c->stream>>>(P);
 }
 
 template <typename R, typename VT, int ENG>
-void launch_iter_q(gqmap_ctx *c, int pipe_n)
+void launch_iter_q(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
 {
     if (c->split == 16)
-        launch_k_iter<R, VT, ENG, 16>(c, pipe_n);
+        launch_k_iter<R, VT, ENG, 16>(c, pipe_n, sg);
     else if (c->split == 4)
-        launch_k_iter<R, VT, ENG, 4>(c, pipe_n);
+        launch_k_iter<R, VT, ENG, 4>(c, pipe_n, sg);
     else
-        launch_k_iter<R, VT, ENG, 1>(c, pipe_n);
+        launch_k_iter<R, VT, ENG, 1>(c, pipe_n, sg);
 }
 
 template <typename R, typename VT>
-void launch_iter_t(gqmap_ctx *c, int pipe_n)
+void launch_iter_t(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
 {
     switch (c->opt.engine) {
-    case GQMAP_ENGINE_SUPER: launch_iter_q<R, VT, 1>(c, pipe_n); break;
-    case GQMAP_ENGINE_CTF: launch_iter_q<R, VT, 2>(c, pipe_n); break;
-    default: launch_iter_q<R, VT, 0>(c, pipe_n); break;
+    case GQMAP_ENGINE_SUPER: launch_iter_q<R, VT, 1>(c, pipe_n, sg); break;
+    case GQMAP_ENGINE_CTF: launch_iter_q<R, VT, 2>(c, pipe_n, sg); break;
+    default: launch_iter_q<R, VT, 0>(c, pipe_n, sg); break;
     }
 }
 
-// pipe_n > 0: one pipelined launch (k_iter_pipe) of pipe_n iterations
-void launch_iter(gqmap_ctx *c, int pipe_n = 0)
+// pipe_n > 0: one pipelined launch (k_iter_pipe) of pipe_n iterations;
+// sg: a subset of the tiles (default: all, one launch)
+void launch_iter(gqmap_ctx *c, int pipe_n = 0, const TileSegs *sg = nullptr)
 {
-    if (c->fp32) launch_iter_t<float, float>(c, pipe_n);
-    else if (c->vv32) launch_iter_t<double, vvs_t>(c, pipe_n);
-    else launch_iter_t<double, double>(c, pipe_n);
+    if (c->fp32) launch_iter_t<float, float>(c, pipe_n, sg);
+    else if (c->vv32) launch_iter_t<double, vvs_t>(c, pipe_n, sg);
+    else launch_iter_t<double, double>(c, pipe_n, sg);
 }
 
 // The pipelined kernel applies when nothing an item reads changes between
@@ -1355,64 +1427,91 @@ struct RcclComm {
 namespace {
 
 template <typename R>
-void halo_copy(gqmap_ctx *c, int col, void *buf, bool to_buf)
+void halo_copy(gqmap_ctx *c, hipStream_t s, int col, uint32_t planes, int np, void *buf, bool to_buf)
 {
-    const int64_t n = (int64_t)NPLANES * c->L * c->M;
+    const int64_t n = (int64_t)np * c->L * c->M;
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
-    k_halo_copy<R><<<grid, 256, 0, c->stream>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M,
-                                                (int64_t)c->M * c->N, c->MNL, c->L, col, (R *)buf, to_buf);
+    k_halo_copy<R><<<grid, 256, 0, s>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M, (int64_t)c->M * c->N,
+                                        c->MNL, c->L, col, planes, np, (R *)buf, to_buf);
 }
 
-void halo_pack(gqmap_ctx *c, int col, void *buf)
+void halo_move(gqmap_ctx *c, hipStream_t s, int col, uint32_t planes, int np, void *buf, bool to_buf)
 {
-    if (c->fp32) halo_copy<float>(c, col, buf, true);
-    else halo_copy<double>(c, col, buf, true);
+    if (c->fp32) halo_copy<float>(c, s, col, planes, np, buf, to_buf);
+    else halo_copy<double>(c, s, col, planes, np, buf, to_buf);
 }
 
-void halo_unpack(gqmap_ctx *c, int col, void *buf)
+// This tile's boundary columns -> d_halo[0] (to the left neighbour) and
+// d_halo[1] (to the right one); d_halo[2] / d_halo[3] (from the left / right
+// neighbour) -> the ghost columns.
+void halo_pack(gqmap_ctx *c, hipStream_t s)
 {
-    if (c->fp32) halo_copy<float>(c, col, buf, false);
-    else halo_copy<double>(c, col, buf, false);
+    if (c->tile > 0) halo_move(c, s, c->own_lo, HALO_TO_LEFT, HALO_TO_LEFT_N, c->d_halo[0], true);
+    if (c->tile < c->n_tiles - 1) halo_move(c, s, c->own_hi - 1, HALO_TO_RIGHT, HALO_TO_RIGHT_N, c->d_halo[1], true);
+}
+void halo_unpack(gqmap_ctx *c, hipStream_t s)
+{
+    if (c->tile > 0) halo_move(c, s, 0, HALO_TO_RIGHT, HALO_TO_RIGHT_N, c->d_halo[2], false);
+    if (c->tile < c->n_tiles - 1) halo_move(c, s, c->N - 1, HALO_TO_LEFT, HALO_TO_LEFT_N, c->d_halo[3], false);
 }
 
-// One iteration on the context's stream.  Whole grid: k_iter + k_finalize.
-// RCCL tile: k_iter, own totals, pack the boundary columns, one RCCL group
-// (in-place all-gather of the totals + ghost-column send/recv with the
-// neighbour ranks), unpack, k_finalize over all tiles' totals.
+// The rest of a whole-grid iteration after k_iter: the finalize, unless the
+// last k_iter workgroup ran it (fused).
 gqmap_status launch_tail(gqmap_ctx *c)
 {
-    if (c->comm) {
-        const int NP = NFIX + c->L, r = c->comm->rank, n = c->comm->nranks;
-        k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)r * NP,
-                                                 c->d_ctl);
-        const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
-        if (left) halo_pack(c, c->own_lo, c->d_halo[0]);
-        if (right) halo_pack(c, c->own_hi - 1, c->d_halo[1]);
-        const size_t cnt = (size_t)NPLANES * c->L * c->M;
-        const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
-        const Rccl *R = rccl();
-        GQ_NCCL(R->GroupStart());
-        GQ_NCCL(R->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
-                             c->comm->comm, c->stream));
-        if (left) {
-            GQ_NCCL(R->Send(c->d_halo[0], cnt, dt, r - 1, c->comm->comm, c->stream));
-            GQ_NCCL(R->Recv(c->d_halo[2], cnt, dt, r - 1, c->comm->comm, c->stream));
-        }
-        if (right) {
-            GQ_NCCL(R->Send(c->d_halo[1], cnt, dt, r + 1, c->comm->comm, c->stream));
-            GQ_NCCL(R->Recv(c->d_halo[3], cnt, dt, r + 1, c->comm->comm, c->stream));
-        }
-        GQ_NCCL(R->GroupEnd());
-        (void)n;
-        if (left) halo_unpack(c, 0, c->d_halo[2]);
-        if (right) halo_unpack(c, c->N - 1, c->d_halo[3]);
+    if (!fused_finalize(c)) launch_finalize(c);
+    return GQMAP_OK;
+}
+
+// One iteration of an RCCL tile.  The boundary tile columns run first; their
+// owned edge columns are packed and sent to the neighbour ranks (grouped
+// ncclSend/ncclRecv over xGMI) on the side stream while the interior tiles
+// run on the context's stream.  Then this tile's exact totals, their
+// all-gather, the received columns into the ghost columns, and the finalize
+// over all tiles' totals (identical on every rank).  e0 / e1 (optional)
+// bracket the two k_iter launches on the main stream.
+gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
+{
+    const int NP = NFIX + c->L, r = c->comm->rank;
+    const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
+    const size_t nl = (size_t)HALO_TO_LEFT_N * c->L * c->M, nr = (size_t)HALO_TO_RIGHT_N * c->L * c->M;
+    const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
+    const Rccl *R = rccl();
+    TileSegs bnd, inr;
+    tile_segments(c, bnd, inr);
+    if (e0) GQ_HIP(hipEventRecord(e0, c->stream));
+    launch_iter(c, 0, &bnd);
+    GQ_HIP(hipEventRecord(c->ev_bnd, c->stream));
+    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_bnd, 0));
+    halo_pack(c, c->side);
+    GQ_NCCL(R->GroupStart());
+    if (left) {
+        GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->side));
+        GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->side));
     }
-    if (!fused_finalize(c)) launch_finalize(c);  // else the last k_iter workgroup did it
+    if (right) {
+        GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->side));
+        GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->side));
+    }
+    GQ_NCCL(R->GroupEnd());
+    launch_iter(c, 0, &inr);
+    if (e1) GQ_HIP(hipEventRecord(e1, c->stream));
+    k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)r * NP,
+                                             c->d_ctl);
+    GQ_HIP(hipEventRecord(c->ev_inr, c->stream));
+    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_inr, 0));
+    GQ_NCCL(R->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
+                         c->comm->comm, c->side));
+    halo_unpack(c, c->side);
+    GQ_HIP(hipEventRecord(c->ev_xch, c->side));
+    GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_xch, 0));
+    launch_finalize(c);
     return GQMAP_OK;
 }
 
 gqmap_status launch_step(gqmap_ctx *c)
 {
+    if (c->comm) return launch_step_rccl(c);
     launch_iter(c);
     return launch_tail(c);
 }
@@ -1544,11 +1643,10 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
         if (s != GQMAP_OK) return s;
         c->have_state = false;
         if (c->n_tiles > 1) {
-            const size_t hb = (size_t)NPLANES * c->L * c->M * c->rsz;
             for (int k = 0; k < 4; ++k) {
                 if (c->d_halo[k]) (void)hipFree(c->d_halo[k]);
                 c->d_halo[k] = nullptr;
-                GQ_HIP(hipMalloc(&c->d_halo[k], hb));
+                GQ_HIP(hipMalloc(&c->d_halo[k], halo_bytes(c, k)));
             }
         }
     }
@@ -2007,6 +2105,11 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     for (int i = 0; i < n_iter;) {
         // pipelined: one launch covers up to PIPE_CHUNK iterations, timed as a whole
         const int n = pipe ? std::min(n_iter - i, PIPE_CHUNK) : 1;
+        if (c->comm) {  // both k_iter launches (boundary, interior) of the iteration
+            if ((s = launch_step_rccl(c, ev[2 + 2 * i], ev[3 + 2 * i])) != GQMAP_OK) return s;
+            i += 1;
+            continue;
+        }
         GQ_HIP(hipEventRecord(ev[2 + 2 * i], c->stream));
         launch_iter(c, pipe ? n : 0);
         GQ_HIP(hipEventRecord(ev[3 + 2 * i], c->stream));
@@ -2174,6 +2277,18 @@ gqmap_status gqmap_create_tile(gqmap_ctx **out, const gqmap_options *opt, int de
     return GQMAP_OK;
 }
 
+// A transport for a tile context: the per-tile totals table [n_tiles][NP].
+static gqmap_status attach_common(gqmap_ctx *c)
+{
+    const size_t NP = NFIX + c->L;
+    GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles));
+    GQ_HIP(hipMemset(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles));
+    c->own_gathered = true;
+    c->nranks = c->n_tiles;
+    drop_graph(c);
+    return GQMAP_OK;
+}
+
 gqmap_status gqmap_comm_unique_id(uint8_t id[128])
 {
     clear_error();
@@ -2192,7 +2307,7 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
     clear_error();
     GQ_CHECK(c && id, GQMAP_ERR_INVALID_ARG, "null argument");
     GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "attach after gqmap_set_images");
-    GQ_CHECK(!c->comm && !c->in_group, GQMAP_ERR_STATE, "tile already has a transport");
+    GQ_CHECK(!c->comm && !c->in_group && !c->host_xfer, GQMAP_ERR_STATE, "tile already has a transport");
     const Rccl *R = rccl();
     GQ_CHECK(R->ok, GQMAP_ERR_UNSUPPORTED, "librccl.so.1 not loadable");
     DeviceGuard dg(c->device);
@@ -2207,13 +2322,100 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
         set_error("ncclCommInitRank(%d ranks, rank %d): %s", c->n_tiles, c->tile, R->GetErrorString(r));
         return GQMAP_ERR_HIP;
     }
-    const size_t NP = NFIX + c->L;
-    GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles));
-    GQ_HIP(hipMemset(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles));
-    c->own_gathered = true;
-    c->nranks = c->n_tiles;
     c->comm = cm;
-    drop_graph(c);
+    gqmap_status s = attach_common(c);
+    if (s != GQMAP_OK) return s;
+    GQ_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    for (hipEvent_t *e : {&c->ev_bnd, &c->ev_inr, &c->ev_xch})
+        GQ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_tile_attach_host(gqmap_ctx *c)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "attach after gqmap_set_images");
+    GQ_CHECK(!c->comm && !c->in_group && !c->host_xfer, GQMAP_ERR_STATE, "tile already has a transport");
+    DeviceGuard dg(c->device);
+    gqmap_status s = attach_common(c);
+    if (s != GQMAP_OK) return s;
+    c->host_xfer = true;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_tile_exchange_sizes(gqmap_ctx *c, size_t sizes[6])
+{
+    clear_error();
+    GQ_CHECK(c && sizes, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "sizes before gqmap_set_images");
+    const size_t NPb = sizeof(fix128) * (NFIX + c->L);
+    const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
+    sizes[0] = left ? halo_bytes(c, 0) : 0;
+    sizes[1] = right ? halo_bytes(c, 1) : 0;
+    sizes[2] = left ? halo_bytes(c, 2) : 0;
+    sizes[3] = right ? halo_bytes(c, 3) : 0;
+    sizes[4] = NPb;
+    sizes[5] = NPb * c->n_tiles;
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_tile_exchange_begin(gqmap_ctx *c, void *send_left, void *send_right, void *totals)
+{
+    clear_error();
+    GQ_CHECK(c && totals, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->host_xfer, GQMAP_ERR_STATE, "gqmap_tile_exchange_begin without gqmap_tile_attach_host");
+    GQ_CHECK(c->have_state, GQMAP_ERR_STATE, "no state");
+    GQ_CHECK((c->tile == 0 || send_left) && (c->tile == c->n_tiles - 1 || send_right), GQMAP_ERR_INVALID_ARG,
+             "tile %d of %d: missing send buffer", c->tile, c->n_tiles);
+    DeviceGuard dg(c->device);
+    const int NP = NFIX + c->L;
+    launch_iter(c);
+    k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)c->tile * NP,
+                                             c->d_ctl);
+    halo_pack(c, c->stream);
+    GQ_HIP(hipGetLastError());
+    if (c->tile > 0)
+        GQ_HIP(hipMemcpyAsync(send_left, c->d_halo[0], halo_bytes(c, 0), hipMemcpyDeviceToHost, c->stream));
+    if (c->tile < c->n_tiles - 1)
+        GQ_HIP(hipMemcpyAsync(send_right, c->d_halo[1], halo_bytes(c, 1), hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipMemcpyAsync(totals, c->d_gathered + (size_t)c->tile * NP, sizeof(fix128) * NP, hipMemcpyDeviceToHost,
+                          c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    return GQMAP_OK;
+}
+
+gqmap_status gqmap_tile_exchange_end(gqmap_ctx *c, const void *recv_left, const void *recv_right,
+                                     const void *totals_all, double *trace3)
+{
+    clear_error();
+    GQ_CHECK(c && totals_all, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->host_xfer, GQMAP_ERR_STATE, "gqmap_tile_exchange_end without gqmap_tile_attach_host");
+    GQ_CHECK((c->tile == 0 || recv_left) && (c->tile == c->n_tiles - 1 || recv_right), GQMAP_ERR_INVALID_ARG,
+             "tile %d of %d: missing receive buffer", c->tile, c->n_tiles);
+    DeviceGuard dg(c->device);
+    const int NP = NFIX + c->L;
+    Ctl h0;
+    gqmap_status s = read_ctl(c, &h0);
+    if (s != GQMAP_OK) return s;
+    if (c->tile > 0)
+        GQ_HIP(hipMemcpyAsync(c->d_halo[2], recv_left, halo_bytes(c, 2), hipMemcpyHostToDevice, c->stream));
+    if (c->tile < c->n_tiles - 1)
+        GQ_HIP(hipMemcpyAsync(c->d_halo[3], recv_right, halo_bytes(c, 3), hipMemcpyHostToDevice, c->stream));
+    GQ_HIP(hipMemcpyAsync(c->d_gathered, totals_all, sizeof(fix128) * NP * c->n_tiles, hipMemcpyHostToDevice,
+                          c->stream));
+    halo_unpack(c, c->stream);
+    launch_finalize(c);
+    GQ_HIP(hipGetLastError());
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    if (trace3) {
+        for (int q = 0; q < 3; ++q) trace3[q] = __builtin_nan("");
+        if (!h0.stop) {
+            Ctl h;
+            if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+            if (h.it > h0.it && (s = fetch_trace(c, h0.it, 1, trace3)) != GQMAP_OK) return s;
+        }
+    }
     return GQMAP_OK;
 }
 
@@ -2229,8 +2431,8 @@ gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n, int n_iter, int *n_d
         GQ_CHECK(c->device == t0->device && c->fp32 == t0->fp32 && c->L == t0->L && c->M == t0->M &&
                      c->Ng == t0->Ng,
                  GQMAP_ERR_INVALID_ARG, "tiles of one group must share device, precision and grid");
-        GQ_CHECK(c->have_images && c->have_state && !c->comm, GQMAP_ERR_STATE,
-                 "tile %d: images/state missing or RCCL attached", t);
+        GQ_CHECK(c->have_images && c->have_state && !c->comm && !c->host_xfer, GQMAP_ERR_STATE,
+                 "tile %d: images/state missing or another transport attached", t);
     }
     DeviceGuard dg(t0->device);
     const int NP = NFIX + t0->L;
@@ -2260,29 +2462,23 @@ gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n, int n_iter, int *n_d
         fetched = ran;
         return r;
     };
-    const size_t hb = (size_t)NPLANES * t0->L * t0->M * t0->rsz;
     for (int i = 0; i < n_iter && s == GQMAP_OK; ++i) {
         for (int t = 0; t < n; ++t) launch_iter(tiles[t]);
         for (int t = 0; t < n; ++t) {
             gqmap_ctx *c = tiles[t];
             k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)t * NP,
                                                      c->d_ctl);
-            if (t > 0) halo_pack(c, c->own_lo, c->d_halo[0]);
-            if (t < n - 1) halo_pack(c, c->own_hi - 1, c->d_halo[1]);
+            halo_pack(c, c->stream);
         }
         for (int t = 0; t < n && s == GQMAP_OK; ++t) {
-            if (t < n - 1 && hipMemcpyAsync(tiles[t + 1]->d_halo[2], tiles[t]->d_halo[1], hb, hipMemcpyDeviceToDevice,
-                                            t0->stream) != hipSuccess)
+            if (t < n - 1 && hipMemcpyAsync(tiles[t + 1]->d_halo[2], tiles[t]->d_halo[1], halo_bytes(t0, 1),
+                                            hipMemcpyDeviceToDevice, t0->stream) != hipSuccess)
                 s = GQMAP_ERR_HIP;
-            if (t > 0 && hipMemcpyAsync(tiles[t - 1]->d_halo[3], tiles[t]->d_halo[0], hb, hipMemcpyDeviceToDevice,
-                                        t0->stream) != hipSuccess)
+            if (t > 0 && hipMemcpyAsync(tiles[t - 1]->d_halo[3], tiles[t]->d_halo[0], halo_bytes(t0, 0),
+                                        hipMemcpyDeviceToDevice, t0->stream) != hipSuccess)
                 s = GQMAP_ERR_HIP;
         }
-        for (int t = 0; t < n; ++t) {
-            gqmap_ctx *c = tiles[t];
-            if (t > 0) halo_unpack(c, 0, c->d_halo[2]);
-            if (t < n - 1) halo_unpack(c, c->N - 1, c->d_halo[3]);
-        }
+        for (int t = 0; t < n; ++t) halo_unpack(tiles[t], tiles[t]->stream);
         for (int t = 0; t < n; ++t) launch_finalize(tiles[t]);
         if (hipGetLastError() != hipSuccess) s = GQMAP_ERR_HIP;
         if (i % 64 == 63 && s == GQMAP_OK) {  // stop test, bounded queue depth, trace drain
@@ -2311,6 +2507,10 @@ void gqmap_destroy(gqmap_ctx *c)
         (void)rccl()->CommDestroy(c->comm->comm);
         delete c->comm;
     }
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    for (hipEvent_t e : {c->ev_bnd, c->ev_inr, c->ev_xch})
+        if (e) (void)hipEventDestroy(e);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);

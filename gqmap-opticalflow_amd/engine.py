@@ -145,6 +145,38 @@ class Engine:
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(unique_id))
         check(self.lib.gqmap_tile_attach_rccl(self.ctx, buf), "gqmap_tile_attach_rccl")
 
+    def attach_host(self) -> None:
+        """Host-staged transport (gqmap_tile_attach_host): the caller moves
+        the boundary columns and totals between exchange_begin / _end."""
+        check(self.lib.gqmap_tile_attach_host(self.ctx), "gqmap_tile_attach_host")
+        sz = (C.c_size_t * 6)()
+        check(self.lib.gqmap_tile_exchange_sizes(self.ctx, sz), "gqmap_tile_exchange_sizes")
+        # send_left, send_right, recv_left, recv_right, totals, totals_all (bytes)
+        self.xfer_sizes = tuple(int(v) for v in sz)
+
+    def exchange_begin(self):
+        """One iteration up to the exchange: (send_left, send_right, totals)
+        as uint8 arrays (send_* empty at the strip ends)."""
+        sl, sr, _, _, tot, _ = self.xfer_sizes
+        bufs = [np.zeros(n, np.uint8) for n in (sl, sr, tot)]
+        ptrs = [b.ctypes.data_as(C.c_void_p) if b.size else None for b in bufs]
+        check(self.lib.gqmap_tile_exchange_begin(self.ctx, *ptrs), "gqmap_tile_exchange_begin")
+        return tuple(bufs)
+
+    def exchange_end(self, recv_left, recv_right, totals_all) -> np.ndarray:
+        """Finish the iteration with the neighbours' columns (recv_left from
+        tile-1's send_right, recv_right from tile+1's send_left) and every
+        tile's totals in tile order.  Returns Energy, ptdmu, ptdsigma."""
+        tr = np.zeros(3)
+        bufs = [np.ascontiguousarray(b, np.uint8) if b is not None else None
+                for b in (recv_left, recv_right, totals_all)]
+        for b, n, what in zip(bufs, self.xfer_sizes[2:4] + self.xfer_sizes[5:], ("recv_left", "recv_right", "totals_all")):
+            if n and (b is None or b.size != n):
+                raise ValueError(f"{what} must hold {n} bytes")
+        ptrs = [b.ctypes.data_as(C.c_void_p) if b is not None and b.size else None for b in bufs]
+        check(self.lib.gqmap_tile_exchange_end(self.ctx, *ptrs, dptr(tr)), "gqmap_tile_exchange_end")
+        return tr
+
     # -- state -----------------------------------------------------------
     def init_state(self, seed: int = 0) -> None:
         check(self.lib.gqmap_init_state(self.ctx, C.c_uint64(seed)), "gqmap_init_state")

@@ -161,8 +161,8 @@ void gqmap_destroy(gqmap_ctx *ctx);
  * The node grid is split into n_tiles strips of whole columns (contiguous in
  * the column-major layout); tile t owns node columns
  * [floor(Ng*t/n), floor(Ng*(t+1)/n)) and keeps one ghost column per
- * neighbour.  Every iteration the tiles exchange their boundary columns (all
- * 9 state planes) and the per-tile exact fixed-point totals (Energy, sums of
+ * neighbour.  Every iteration the tiles exchange their boundary columns (the
+ * state planes the neighbour reads) and the per-tile exact fixed-point totals (Energy, sums of
  * |dmu|, |dsigma|, dalpha), so a tiled solve is bit-identical to the whole-
  * grid solve (§8(e) of SURVEY.md: gqmap_gpu_mixture.m:29-46 is Jacobi).
  * A tile context takes the FULL frames in gqmap_set_images (replicated: the
@@ -182,6 +182,26 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *ctx, const uint8_t id[128]);
  * trace as gqmap_run (tile 0's copy; every tile computes the same). */
 gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n_tiles, int n_iter, int *n_done,
                                   double *trace);
+/* Host-staged transport, for callers that move the boundary data themselves
+ * (MPI between nodes, sockets, torch.distributed gloo; one process per tile,
+ * any device).  One iteration is
+ *   gqmap_tile_exchange_begin: the iteration kernel, this tile's exact totals
+ *       and its boundary columns, copied out to host buffers;
+ *   the caller sends send_left to tile-1 (its recv_right) and send_right to
+ *       tile+1 (its recv_left), and all-gathers the totals in tile order;
+ *   gqmap_tile_exchange_end: the received columns into the ghost columns, the
+ *       finalize over all tiles' totals; trace3 (optional) = Energy, ptdmu,
+ *       ptdsigma of the iteration (NaN once the run has stopped).
+ * The boundary messages carry only what the neighbour reads: 4 planes (mu,
+ * sigma) leftwards, 6 (mu, sigma, rou of the right edges) rightwards.
+ * gqmap_tile_exchange_sizes: bytes of send_left, send_right, recv_left,
+ * recv_right (0 at the strip ends), one tile's totals, all tiles' totals.  The RCCL path above is the
+ * same exchange on the device (gqmap_gpu_mixture.m:29-46, 69-75). */
+gqmap_status gqmap_tile_attach_host(gqmap_ctx *ctx);
+gqmap_status gqmap_tile_exchange_sizes(gqmap_ctx *ctx, size_t sizes[6]);
+gqmap_status gqmap_tile_exchange_begin(gqmap_ctx *ctx, void *send_left, void *send_right, void *totals);
+gqmap_status gqmap_tile_exchange_end(gqmap_ctx *ctx, const void *recv_left, const void *recv_right,
+                                     const void *totals_all, double *trace3);
 
 /* ---- standalone device ops (host pointers in/out) ---- */
 /* projsplx.m:15-30, applied independently to each of `ncols` columns of Y

@@ -166,3 +166,45 @@ def test_tile_group_long_run_trace_drained():
     finally:
         for t in tiles:
             t.close()
+
+
+def test_host_staged_tiles_three_processes_bit_exact(tmp_path):
+    """Three processes share cuda:0, each holding one column-strip tile of
+    libgqmap (L=3 mixture, alpha update and temperature decay inside the
+    run).  Boundary columns (4 planes leftwards, 6 rightwards) and exact
+    totals travel through torch.distributed gloo between
+    gqmap_tile_exchange_begin and _end -- the library's own pack / unpack and
+    cross-process finalize, as a multi-node MPI caller would drive them.
+    Bit-identical to the whole-grid solve."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    I1, I2, o = _problem("mixture", 3, 96, 128)
+    its, world = 30, 3
+    init, ref, tr = _whole(I1, I2, o, "mixture", "fp64", its, seed=3)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    procs = [subprocess.Popen([sys.executable, "-m", "tests._tile_host_worker", str(r), str(world), str(port),
+                               str(its), str(tmp_path / f"r{r}.npz")], cwd=root, env=env)
+             for r in range(world)]
+    try:
+        for p in procs:
+            assert p.wait(timeout=200) == 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    cols = []
+    for r in range(world):
+        d = np.load(tmp_path / f"r{r}.npz")
+        c0, c1 = int(d["col0"]), int(d["col1"])
+        cols.append((c0, c1))
+        np.testing.assert_array_equal(d["trace"], tr, err_msg=f"rank {r} trace")
+        for k in ("muu", "muv", "sigu", "sigv", "pn", "rou"):
+            np.testing.assert_array_equal(d[k], getattr(ref, k)[:, c0:c1], err_msg=f"rank {r} {k}")
+        np.testing.assert_array_equal(d["alpha"], ref.alpha)
+    assert cols[0][0] == 0 and cols[-1][1] == ref.muu.shape[1]

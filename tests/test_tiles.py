@@ -117,28 +117,33 @@ def _gloo_worker(rank, world, port, its, result_q):
         import torch
         for it in range(1, its + 1):
             _, _, T, totals = oracle.emu_run_tile(o, I1, I2, s, it, 1, X, W, (n_off, lo, hi, N), T=T)
-            # ghost columns <- the neighbours' boundary columns (all 9 planes)
-            arrs = s.arrays()[:6]
-            pack = lambda c: torch.from_numpy(np.concatenate([a[:, c].ravel(order="F") for a in arrs]))
-            def unpack(c, buf):
+            # ghost columns <- the neighbours' boundary columns: only what the
+            # library ships (gqmap_engine.hip HALO_TO_LEFT / HALO_TO_RIGHT):
+            # mu, sigma leftwards; mu, sigma and rou of the right edges
+            # (dir 2, u and v) rightwards.  pn / rou(dir 1) of a ghost stay stale.
+            muu, muv, sigu, sigv, _, rou = s.arrays()[:6]
+            views = lambda c, right: ([muu[:, c], muv[:, c], sigu[:, c], sigv[:, c]] +
+                                      ([rou[:, c, :, 1, 0], rou[:, c, :, 1, 1]] if right else []))
+            pack = lambda c, right: torch.from_numpy(np.concatenate([v.ravel(order="F") for v in views(c, right)]))
+            def unpack(c, right, buf):
                 off = 0
-                for a in arrs:
-                    n = a[:, c].size
-                    a[:, c] = buf[off:off + n].numpy().reshape(a[:, c].shape, order="F")
+                for v in views(c, right):
+                    n = v.size
+                    v[...] = buf[off:off + n].numpy().reshape(v.shape, order="F")
                     off += n
             reqs, bufs = [], {}
             if rank > 0:
-                bufs["l"] = torch.empty_like(pack(lo))
-                reqs += [dist.isend(pack(lo), rank - 1), dist.irecv(bufs["l"], rank - 1)]
+                bufs["l"] = torch.empty_like(pack(0, True))
+                reqs += [dist.isend(pack(lo, False), rank - 1), dist.irecv(bufs["l"], rank - 1)]
             if rank < world - 1:
-                bufs["r"] = torch.empty_like(pack(hi - 1))
-                reqs += [dist.isend(pack(hi - 1), rank + 1), dist.irecv(bufs["r"], rank + 1)]
+                bufs["r"] = torch.empty_like(pack(Nl - 1, False))
+                reqs += [dist.isend(pack(hi - 1, True), rank + 1), dist.irecv(bufs["r"], rank + 1)]
             for r in reqs:
                 r.wait()
             if "l" in bufs:
-                unpack(0, bufs["l"])
+                unpack(0, True, bufs["l"])
             if "r" in bufs:
-                unpack(Nl - 1, bufs["r"])
+                unpack(Nl - 1, False, bufs["r"])
             # per-tile exact totals -> every rank sums all of them
             allt = [None] * world
             dist.all_gather_object(allt, totals)
