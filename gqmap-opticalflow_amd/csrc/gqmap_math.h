@@ -462,14 +462,22 @@ GQ_HD void spectral_st(R p, R &s, R &t)
 
 // Epilogue shared by node (tau = -3T) and edge (tau = +T) gradients
 // (gqmap_gpu_mixture.m:107-115 and :137-145).  lam = -lambda scales the sums.
+//
+// The reference divides by pi in six places; here 1/pi is folded into the
+// sums' scale (lam/pi: one multiply per sum, six correctly rounded divisions
+// fewer per node / edge gradient).  Each quotient differs from the
+// reference's by a rounding or two (the literal restatement in oracle/ keeps
+// the reference's order; the tests hold the two within 1e-12 per step).
+// Replacing the remaining divisions by o1, o2, pr with reciprocals measured
+// 13% slower on C2 fp64 (fp32 2% faster) and is not used.
 template <typename R>
 GQ_HD Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s, R t, R tau,
                        bool live, bool raw_energy = false)
 {
-    const R pi = R(GQ_M_PI);
     const R c1 = R(2.8378770664093454835606594728112);  // 1 + log(2*pi)
-    const R S0 = lam * S.s0, Sxi = lam * S.sxi, Sxj = lam * S.sxj;
-    const R Sa = lam * S.sa, Sm = lam * S.sm, Sx = lam * S.sx;
+    const R lp = lam * R(1.0 / GQ_M_PI);
+    const R S0 = lp * S.s0, Sxi = lp * S.sxi, Sxj = lp * S.sxj;
+    const R Sa = lp * S.sa, Sm = lp * S.sm, Sx = lp * S.sx;
     const R pr = R(1) - p * p;
     const R sqrtpr = GQ_SQRT(pr);
     const R a1 = s - p * t, a2 = t - p * s;
@@ -482,15 +490,15 @@ GQ_HD Grad<R> epilogue(const Sums<R> &S, R lam, R a, R o1, R o2, R p, R s, R t, 
     if (!live) dp = du1 = du2 = do1 = do2 = R(0);
     Grad<R> g;
     const R sq2 = R(GQ_M_SQRT2);
-    g.du1 = a * du1 * (sq2 / (o1 * pr)) / pi;
-    g.du2 = a * du2 * (sq2 / (o2 * pr)) / pi;
+    g.du1 = a * du1 * (sq2 / (o1 * pr));
+    g.du2 = a * du2 * (sq2 / (o2 * pr));
     const R ent = tau != R(0) ? tau * (c1 + gq_logr<R>(sqrtpr * o1 * o2)) : R(0);
-    g.da = S0 / pi + ent;
-    g.do1 = a * (do1 / pi + tau) / o1;
-    g.do2 = a * (do2 / pi + tau) / o2;
-    g.dp = a * (dp / pi - tau * p) / pr;
+    g.da = S0 + ent;
+    g.do1 = a * (do1 + tau) / o1;
+    g.do2 = a * (do2 + tau) / o2;
+    g.dp = a * (dp - tau * p) / pr;
     // gqmap_ctf.m's nener/eener = -lambda*sum(fval): no 1/pi, no alpha
-    g.E = raw_energy ? S0 : a * g.da;
+    g.E = raw_energy ? lam * S.s0 : a * g.da;
     return g;
 }
 
