@@ -153,10 +153,22 @@ def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 8.0
 
 
 def traffic_per_launch(precision: str, config: str):
+    """HBM bytes per k_iter launch from the committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes (scripts/profile_round.sh -> profiles/traffic_*.json):
+    counter collection needs its own profiler runs, so it is not measured
+    inside the timed bench."""
     tfile = os.path.join(ROOT, "profiles", f"traffic_{config}_{precision}.json")
     if os.path.exists(tfile):
         return json.load(open(tfile)).get("hbm_bytes_per_launch")
     return None
+
+
+def traffic_source(precision: str, config: str):
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{config}_{precision}.json")
+    if not os.path.exists(tfile):
+        return None
+    d = json.load(open(tfile))
+    return f"profiles/traffic_{config}_{precision}.json ({d.get('source', 'rocprofv3 FETCH_SIZE+WRITE_SIZE passes')})"
 
 
 def roofline(engine, L, K, nodes, precision, kernel_avg_s, config, kernel_name):
@@ -166,7 +178,8 @@ def roofline(engine, L, K, nodes, precision, kernel_avg_s, config, kernel_name):
     ach = fl / kernel_avg_s / 1e12
     peak = PEAK_TFLOPS[precision]
     return {"bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
-            "traffic": traffic_per_launch(precision, config), "kernel": kernel_name,
+            "traffic": traffic_per_launch(precision, config), "traffic_source": traffic_source(precision, config),
+            "kernel": kernel_name,
             "kernel_avg_us": kernel_avg_s * 1e6, "flops_per_launch": fl,
             "algorithmic_bytes_per_launch": by, "hbm_algorithmic_GBps": by / kernel_avg_s / 1e9,
             "hbm_frac": by / kernel_avg_s / 1e9 / PEAK_HBM_GBPS}
@@ -450,6 +463,9 @@ def main():
                     + ("; upsampled 4x on the device" if cfg == "c5" else ""),
             "config": {"workload": r["workload"], "engine": engine, "L": L, "K": K, "parallelism": parallel},
             "aepe": r["aepe"], "aepe_its": args.steps,
+            "timed_region": "iterations 1..steps of the solve (gqmap_gpu_mixture.m:27-50, 69-75 on the device); "
+                            "the reference loop's host evaluation block (it==1 / every 300 its: MAP, PNG, AEPE, "
+                            "logP, :52-68) is outside it -- aepe is computed once after the timed steps",
         }
         if cfg == "c1":
             # per pixel: node 2 x K x 6 flop, edges 4 x K^2 x ~40 flop (legacy/gqmap_cpu.m:20-54)

@@ -79,14 +79,8 @@ __device__ __forceinline__ float gq_sqrt_dev(float x)
 #ifndef GQ_NODE_UNROLL_N
 #define GQ_NODE_UNROLL_N 1
 #endif
-#ifndef GQ_PIPE_FENCES  // 1: release/acquire fences around tile hand-offs; 0: sc1 stores + sc1 loads
-#define GQ_PIPE_FENCES 0
-#endif
 #ifndef GQ_VV16  // experiment: exact-integer frames stored as _Float16 instead of float (fp64 engine)
 #define GQ_VV16 0
-#endif
-#ifndef GQ_PIPE_STATS  // instrumentation builds only: dependency-wait / busy cycles of the pipelined kernel
-#define GQ_PIPE_STATS 0
 #endif
 #ifndef GQ_FIN_GROUP
 #define GQ_FIN_GROUP 1  // finalize: the NFIX fixed sums loaded together (fp32 C2 -2 us)
@@ -134,13 +128,6 @@ struct Ctl {
     int done;  // completed iterations since the state was set (ping-pong parity)
     int stop;  // ptdmu < tor reached
     int arrive;  // fused finalize: workgroups done with this iteration
-    // pipelined kernel (k_iter_pipe): work queue, the launch's first
-    // iteration and completed count, last finalized iteration, arrival
-    // tickets of the two iterations in flight
-    int queue, launch_it, launch_done, fin_it;
-    int arrive2[2];
-    // GQ_PIPE_STATS builds: cycles spent waiting for dependencies / in tiles, items
-    unsigned long long st_wait, st_busy, st_items;
     double T;
     double alpha[GQMAP_LMAX];
     double w[GQMAP_LMAX];
@@ -403,47 +390,9 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
     return tile;
 }
 
-// State store of the update: plain, or (PIPE) a device-coherent write-through
-// store -- the pipelined kernel hands tiles to other workgroups in-launch.
-template <bool PIPE, typename R>
-__device__ __forceinline__ void put_state(R *p, R v)
-{
-    if (PIPE) {
-        if (sizeof(R) == 8) {
-            uint64_t u;
-            __builtin_memcpy(&u, &v, 8);
-            __hip_atomic_store(reinterpret_cast<uint64_t *>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            uint32_t u;
-            __builtin_memcpy(&u, &v, 4);
-            __hip_atomic_store(reinterpret_cast<uint32_t *>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else {
-        *p = v;
-    }
-}
-
-// State load: plain, or (PIPE without fences) a device-coherent sc1 load.
-template <bool PIPE, typename R>
-__device__ __forceinline__ R get_state(const R *p)
-{
-    if (PIPE && !GQ_PIPE_FENCES) {
-        if (sizeof(R) == 8) {
-            const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            R v;
-            __builtin_memcpy(&v, &u, 8);
-            return v;
-        } else {
-            const uint32_t u = __hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            R v;
-            __builtin_memcpy(&v, &u, 4);
-            return v;
-        }
-    }
-    return *p;
-}
+// Node rows of a tile with Q lanes per node (256 / Q nodes): 16 x 16, 16 x 8
+// (two 16-row columns per wave), 8 x 8, 4 x 4; lanes are m-fastest.
+constexpr int tile_rows(int q) { return q <= 2 ? 16 : q == 4 ? 8 : 4; }
 
 // LDS of one tile: in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n);
 // in_left: from (m,n-1); red: per-wave partial sums.  Declared by the kernels
@@ -461,13 +410,13 @@ struct TileLds {
 // One tile of one iteration (absolute iteration `it`, reading state buffer
 // `parity`): node and edge gradients, neighbour scatter, clamped ascent into
 // the other buffer, and the tile's exact partial sums into part_row[0..NP).
-template <typename R, typename VT, int ENG, int Q, bool PIPE, bool EDGE_FIRST>
+template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
                                           fix128 *part_row, TileLds<R, BLOCK / Q> &lds, int l0, int l1)
 {
     constexpr int TPIX = BLOCK / Q;                   // nodes per tile
-    constexpr int TM = Q == 1 ? 16 : Q == 4 ? 8 : 4;  // tile side
-    static_assert(TM * TM == TPIX, "tile");
+    constexpr int TM = tile_rows(Q), TN = TPIX / TM;  // tile rows x columns
+    static_assert(TM * TN == TPIX, "tile");
     Ctl *ctl = P.ctl;
     const R *__restrict__ src = parity ? P.st1 : P.st0;
     R *__restrict__ dst = parity ? P.st0 : P.st1;
@@ -478,7 +427,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     const int tid = threadIdx.x;
     const int pix = tid / Q, kj = tid % Q;  // node within the tile, lane within the node
     const int lm = pix % TM, ln = pix / TM;
-    const int m0 = tm * TM, n0 = tn * TM;
+    const int m0 = tm * TM, n0 = tn * TN;
     const int m = m0 + lm, n = n0 + ln;
     const int M = P.M, N = P.N;
     const int64_t MNL = P.MNL, MN = (int64_t)M * N;
@@ -508,8 +457,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     fix128 fE = 0, fmu = 0, fsg = 0, fae = 0;
     int nonfinite = 0;
     const int wave = tid >> 6, lane = tid & 63;
-    // halo: 4*TM edges (top row and left column, u and v) x Q lanes, whole waves
-    constexpr int HALO_LANES = 4 * TM * Q;
+    // halo: 2*(TN+TM) edges (top row and left column, u and v) x Q lanes
+    constexpr int HALO_LANES = 2 * (TN + TM) * Q;
     const bool halo_lane = tid < HALO_LANES;
 
     for (int l = l0; l < l1; ++l) {
@@ -519,11 +468,11 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // are read and updated by their edge jobs.  (Named scalars, not an
         // array: a select between two array elements by the run-time uv
         // below would put the array in scratch.)
-        const R mu_u = valid ? get_state<PIPE>(&src[i]) : R(0);
-        const R mu_v = valid ? get_state<PIPE>(&src[i + MNL]) : R(0);
-        const R sg_u = valid ? get_state<PIPE>(&src[i + MNL * 2]) : R(0);
-        const R sg_v = valid ? get_state<PIPE>(&src[i + MNL * 3]) : R(0);
-        const R pn = valid ? get_state<PIPE>(&src[i + MNL * 4]) : R(0);
+        const R mu_u = valid ? src[i] : R(0);
+        const R mu_v = valid ? src[i + MNL] : R(0);
+        const R sg_u = valid ? src[i + MNL * 2] : R(0);
+        const R sg_v = valid ? src[i + MNL * 3] : R(0);
+        const R pn = valid ? src[i + MNL * 4] : R(0);
         Grad<R> nd{};
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R eE = 0, eda = 0;                                     // sum over the 4 edges
@@ -565,9 +514,10 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                 rm = dir == 0 ? m + 1 : m; rn = dir == 1 ? n + 1 : n;
             } else {
                 const int h = tid / Q;  // halo edge index
-                const bool top = h < 2 * TM;
-                uv = (h / TM) & 1;
-                hr = h % TM;
+                const bool top = h < 2 * TN;
+                const int hh = top ? h : h - 2 * TN, span = top ? TN : TM;
+                uv = hh / span;
+                hr = hh % span;
                 dir = top ? 0 : 1;
                 hm = top ? m0 - 1 : m0 + hr; hn = top ? n0 + hr : n0 - 1;
                 rm = top ? m0 : hm;          rn = top ? hn : n0;
@@ -578,18 +528,18 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             if (need) {
                 const int64_t h = hm + (int64_t)M * hn + MN * l;
                 const int64_t r = rm + (int64_t)M * rn + MN * l;
-                const R u1 = own_edge ? (uv ? mu_v : mu_u) : get_state<PIPE>(&src[h + MNL * uv]);
-                const R o1 = own_edge ? (uv ? sg_v : sg_u) : get_state<PIPE>(&src[h + MNL * (2 + uv)]);
-                const R p = get_state<PIPE>(&src[h + MNL * (5 + dir + 2 * uv)]);  // rou plane 5+e
-                const R o2 = get_state<PIPE>(&src[r + MNL * (2 + uv)]);
-                const EdgeCoef<R> c = edge_coef(u1, get_state<PIPE>(&src[r + MNL * uv]), o1, o2, p);
+                const R u1 = own_edge ? (uv ? mu_v : mu_u) : src[h + MNL * uv];
+                const R o1 = own_edge ? (uv ? sg_v : sg_u) : src[h + MNL * (2 + uv)];
+                const R p = src[h + MNL * (5 + dir + 2 * uv)];  // rou plane 5+e
+                const R o2 = src[r + MNL * (2 + uv)];
+                const EdgeCoef<R> c = edge_coef(u1, src[r + MNL * uv], o1, o2, p);
                 Sums<R> S = edge_sums(tab, kj, K2, Q, P.epsn, c);
                 if (Q > 1) S = lane_combine<Q>(S);
                 g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p, ENG == 2);
                 // the edge owns its correlation: clamped ascent right here
                 // (gqmap_gpu_mixture.m:46), nothing else reads drou
                 if (own_edge && inner && lead)
-                    put_state<PIPE, R>(&dst[i + MNL * (5 + e)], fmin(fmax(p + g.dp * step, -P.corr), P.corr));
+                    dst[i + MNL * (5 + e)] = fmin(fmax(p + g.dp * step, -P.corr), P.corr);
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
@@ -598,7 +548,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                 eda = eda + g.da;
                 // neighbour share: (m+1,n) reads in_up, (m,n+1) reads in_left
                 if (lead && dir == 0 && lm + 1 < TM) { in_up[uv][0][pix + 1] = g.du2; in_up[uv][1][pix + 1] = g.do2; }
-                if (lead && dir == 1 && ln + 1 < TM) { in_left[uv][0][pix + TM] = g.du2; in_left[uv][1][pix + TM] = g.do2; }
+                if (lead && dir == 1 && ln + 1 < TN) { in_left[uv][0][pix + TM] = g.du2; in_left[uv][1][pix + TM] = g.do2; }
             } else if (tid % Q == 0) {
                 if (dir == 0) { in_up[uv][0][hr * TM] = g.du2; in_up[uv][1][hr * TM] = g.do2; }
                 else          { in_left[uv][0][hr] = g.du2; in_left[uv][1][hr] = g.do2; }
@@ -616,8 +566,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
             auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
             const R nu = cl(mu_u + gmu_u * step, P.minu, P.maxu), nv = cl(mu_v + gmu_v * step, P.minv, P.maxv);
-            put_state<PIPE, R>(&dst[i + MNL * 0], nu);
-            put_state<PIPE, R>(&dst[i + MNL * 1], nv);
+            dst[i + MNL * 0] = nu;
+            dst[i + MNL * 1] = nv;
             if constexpr (ENG == 2) {  // AEPE of gqmap_ctf.m:38 against the updated mean
                 if (P.truth) {
                     const double du = P.truth[m + (int64_t)M * n] - (double)nu;
@@ -628,9 +578,9 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
             const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
             const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
-            put_state<PIPE, R>(&dst[i + MNL * 2], cl(sg_u + su, P.sig_lo, P.sig_hi));
-            put_state<PIPE, R>(&dst[i + MNL * 3], cl(sg_v + sv, P.sig_lo, P.sig_hi));
-            put_state<PIPE, R>(&dst[i + MNL * 4], cl(pn + nd.dp * step, -P.corr, P.corr));
+            dst[i + MNL * 2] = cl(sg_u + su, P.sig_lo, P.sig_hi);
+            dst[i + MNL * 3] = cl(sg_v + sv, P.sig_lo, P.sig_hi);
+            dst[i + MNL * 4] = cl(pn + nd.dp * step, -P.corr, P.corr);
             // per-node contributions to the global sums (exact fixed point)
             const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
             const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
@@ -703,9 +653,9 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
     __shared__ TileLds<R, BLOCK / Q> lds;
     fix128 *part_row = P.partials + (int64_t)(P.part_off + b) * NP;
     if (edge_first)
-        iter_tile<R, VT, ENG, Q, false, true>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, true>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
     else
-        iter_tile<R, VT, ENG, Q, false, false>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, false>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
 #if GQ_TIMELINE
     __syncthreads();
     if (threadIdx.x == 0 && ctl->it == GQ_TIMELINE && b < 8192) {
@@ -740,183 +690,6 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
         ctl->arrive = 0;
     }
 }
-
-// ---------------------------------------------------------------------------
-// pipelined iteration kernel
-//
-// One launch runs n_iter iterations.  Its workgroups take items (iteration j,
-// tile) from one device-wide queue in (j, tile) order; an item waits only for
-// the tiles it reads -- itself and its 4 neighbour tiles -- to have finished
-// iteration j-1 (per-tile counters), so iteration j+1 starts on one part of
-// the frame while iteration j drains elsewhere: no per-launch fill and drain,
-// no tail.  The update is Jacobi with two state buffers, and a tile of
-// iteration j+1 overwrites buffer (j+1)&1 = (j-1)&1 only after its neighbours
-// finished reading it in iteration j (the same counters).  Partial sums go to
-// one of two slots (j&1); the last tile of iteration j runs its finalize
-// after that of j-1.  Items of iteration j wait for the finalize of j-2: a
-// stop (ptdmu < tor) at iteration s lets at most iteration s+1 run
-// speculatively, into the buffer that held s-1, and is then discarded --
-// the state of iteration s stays intact.  Used when nothing the items read
-// changes between iterations (L = 1, constant temperature): alpha, T and the
-// step (a function of it) are then fixed per item.
-//
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): state and
-// partials are stored write-through (sc1); every wave drains its stores,
-// the workgroup meets at a barrier, lane 0 releases at agent scope and then
-// publishes the tile counter / takes the arrival ticket; a consumer polls
-// with sc1 loads, acquires at agent scope, and its waves pass a barrier
-// before reading.  The queue is only popped by running workgroups, so an
-// item never waits for one that has not been handed out: no deadlock for any
-// grid size or residency.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int ld_agent(const int *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(int *p, int v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Spin until *p >= v; false if the run stopped meanwhile (a stop at
-// iteration s is set after every item of s completed, so whoever still waits
-// belongs to a discarded iteration > s).
-__device__ __forceinline__ bool wait_ge(const int *p, int v, const int *stop)
-{
-    while (ld_agent(p) < v) {
-        if (ld_agent(stop)) return false;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return true;
-}
-
-// Before each pipelined launch (all earlier work is complete at a launch
-// boundary): reset the queue and tickets, every tile counter and the
-// finalize counter to "iteration it-1 done".
-__global__ void k_pipe_prep(Ctl *ctl, int *done_it, int nb)
-{
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int it = ctl->it;
-    if (i < nb) done_it[i] = it - 1;
-    if (i == 0) {
-        ctl->queue = 0;
-        ctl->arrive2[0] = ctl->arrive2[1] = 0;
-        ctl->launch_it = it;
-        ctl->launch_done = ctl->done;
-        ctl->fin_it = it - 1;
-        ctl->st_wait = ctl->st_busy = ctl->st_items = 0;
-    }
-}
-
-// The finalizer workgroup of the pipelined kernel (block 0: dispatched
-// first, so it is resident whatever the residency of the grid): iteration by
-// iteration, wait until every tile has arrived, reduce the partials, apply
-// the finalize step, re-arm the ticket and publish fin_it.  A workgroup of
-// its own keeps this code out of the item loop (inlined there it raised the
-// loop's register allocation by a wave per SIMD).
-__device__ void pipe_finalizer(const FinParams &F0, fix128 *partials, int nb, int NP, int it0, int n_iter,
-                               double *tot, fix128 *sh_red, int *sh_ok)
-{
-    Ctl *ctl = F0.ctl;
-    const int tid = threadIdx.x;
-    for (int j = 0; j < n_iter; ++j) {
-        const int it = it0 + j;
-        if (tid == 0) {
-            // stop is only ever set by this loop: no wait can miss it
-            *sh_ok = !ld_agent(&ctl->stop) && wait_ge(&ctl->arrive2[it & 1], nb, &ctl->stop);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        if (!*sh_ok) return;
-        FinParams F = F0;
-        F.partials = partials + (int64_t)(it & 1) * nb * NP;
-        F.nblocks = nb;
-        fin_reduce(F, tot, sh_red);
-        if (tid == 0) {
-            fin_apply(F, tot);
-            st_agent(&ctl->arrive2[it & 1], 0);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st_agent(&ctl->fin_it, it);
-        }
-        __syncthreads();
-    }
-}
-
-template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter_pipe(IterParams<R, VT> P, int n_iter,
-                                                                   int *done_it)
-{
-    Ctl *ctl = P.ctl;
-    const int nb = P.tiles_m * P.tiles_n;
-    const int NP = NFIX + P.L;
-    const int tid = threadIdx.x;
-    const int it0 = ctl->launch_it, done0 = ctl->launch_done;  // set by k_pipe_prep
-    const int64_t items = (int64_t)n_iter * nb;
-    __shared__ int sh_item;
-    __shared__ TileLds<R, BLOCK / Q> lds;
-    if (blockIdx.x == 0) {
-        __shared__ double tot[NFIX + GQMAP_LMAX];
-        __shared__ fix128 sh_red[256];
-        pipe_finalizer(P.fin, P.partials, nb, NP, it0, n_iter, tot, sh_red, &sh_item);
-        return;
-    }
-    for (int k = 0;; ++k) {
-#if GQ_PIPE_STATS
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
-        if (tid == 0) {
-            int item = -1;
-            const int q = atomicAdd(&ctl->queue, 1);
-            if (q < items) {
-                const int j = q / nb, tile = q % nb, it = it0 + j;
-                const int *stop = &ctl->stop, tm = tile % P.tiles_m, tn = tile / P.tiles_m;
-                // the stop decision of iteration it-2, then the tiles this item reads
-                bool ok = wait_ge(&ctl->fin_it, it - 2, stop) && !ld_agent(stop);
-                ok = ok && wait_ge(&done_it[tile], it - 1, stop);
-                ok = ok && (tm == 0 || wait_ge(&done_it[tile - 1], it - 1, stop));
-                ok = ok && (tm + 1 == P.tiles_m || wait_ge(&done_it[tile + 1], it - 1, stop));
-                ok = ok && (tn == 0 || wait_ge(&done_it[tile - P.tiles_m], it - 1, stop));
-                ok = ok && (tn + 1 == P.tiles_n || wait_ge(&done_it[tile + P.tiles_m], it - 1, stop));
-                if (ok) item = q;
-            }
-            if (GQ_PIPE_FENCES) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            sh_item = item;
-        }
-        __syncthreads();
-        const int q = sh_item;
-        if (q < 0) break;  // queue drained or the run stopped
-#if GQ_PIPE_STATS
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-#endif
-        const int j = q / nb, tile = q % nb, it = it0 + j;
-        // phase order alternates between consecutive items of a workgroup
-        const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((int)blockIdx.x + k) & 1);
-        fix128 *slot = P.partials + (int64_t)(it & 1) * nb * NP;
-        if (edge_first)
-            iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds, 0, P.L);
-        else
-            iter_tile<R, VT, ENG, Q, true, false>(P, tile, it, (done0 + j) & 1, slot + (int64_t)tile * NP, lds, 0, P.L);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            if (GQ_PIPE_FENCES) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st_agent(&done_it[tile], it);
-            atomicAdd(&ctl->arrive2[it & 1], 1);
-#if GQ_PIPE_STATS
-            const unsigned long long t2 = __builtin_amdgcn_s_memtime();
-            atomicAdd(&ctl->st_wait, t1 - t0);
-            atomicAdd(&ctl->st_busy, t2 - t1);
-            atomicAdd(&ctl->st_items, 1ull);
-#endif
-        }
-        __syncthreads();
-    }
-}
-
-
 
 __global__ __launch_bounds__(256) void k_finalize(FinParams F)
 {
@@ -1090,7 +863,6 @@ struct gqmap_ctx {
     double *d_trace = nullptr;
     double *d_truth = nullptr;  // gqmap_set_truth: M x N x 2 (ctf engine)
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
-    int *d_done_it = nullptr;  // pipelined kernel: per-tile completed iteration
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
     int split = 1;      // lanes per node (Q): 1, 4 or 16
@@ -1124,18 +896,19 @@ namespace {
 // Lanes per node Q (a node's quadrature split over Q lanes of one wave: more
 // lanes in flight; the lane-varying table index is served from an LDS copy of
 // the quadrature table).  Measured per-iteration k_iter times (scripts/
-// level_sweep.py, ctf engine K=11, us for Q = 1 / 4 / 16): 30x40 102/48/35,
-// 60x80 103/48/45, 120x160 108/72/99, 240x320 158/161/329, 480x640
-// 309/467/1170 -> single-pixel engines: Q = 16 below 2^13 nodes, 4 below
-// 2^16, else 1.  The super engine runs its L components as separate blocks
+// level_sweep.py, ctf engine K=11, us for Q = 1 / 2 / 4 / 16, round 2):
+// 30x40 109/81/53/34, 60x80 112/83/54/43, 120x160 113/87/67/100, 240x320
+// 173/142/145/332, 480x640 302/374/423/1207; C2 (mixture K=9, 388x584)
+// Q=1 173, Q=2 227 -> single-pixel engines: Q = 16 below 2^13 nodes, 4
+// below 2^16, 2 below 2^17, else 1.  The super engine runs its L components as separate blocks
 // (choose_lpar) and counts node-components: C4 (120x160 x L=3 = 57,600)
 // Q = 16 / 4 / 1 -> 616 / 509 / 613-717 us with global table reads (one block
 // per tile: 680 / 829 / 1687); Q = 4 with the LDS table 376 us.
 int choose_split(int M, int N, int L, int forced, bool super_)
 {
-    if (forced == 1 || forced == 4 || forced == 16) return forced;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 16) return forced;
     const int64_t nodes = (int64_t)M * N;
-    if (!super_) return nodes >= (1 << 16) ? 1 : nodes >= (1 << 13) ? 4 : 16;
+    if (!super_) return nodes >= (1 << 17) ? 1 : nodes >= (1 << 16) ? 2 : nodes >= (1 << 13) ? 4 : 16;
     const int64_t nl = nodes * L;
     if (nl >= (1 << 17)) return 1;
     if (nl >= (1 << 14)) return 4;
@@ -1166,9 +939,9 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     // from the whole grid (Ng columns), so every column-strip tile sums its
     // quadrature in the same order as the untiled solve
     c->split = choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
-    const int tile = c->split == 1 ? 16 : c->split == 4 ? 8 : 4;
-    c->tiles_m = (c->M + tile - 1) / tile;
-    c->tiles_n = (c->N + tile - 1) / tile;
+    const int tr = tile_rows(c->split), tc = BLOCK / c->split / tr;
+    c->tiles_m = (c->M + tr - 1) / tr;
+    c->tiles_n = (c->N + tc - 1) / tc;
     c->lpar = choose_lpar(c);
     c->nblocks = c->tiles_m * c->tiles_n * c->lpar;
     const size_t bytes = (size_t)c->MNL * NPLANES * c->rsz;
@@ -1179,11 +952,7 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     }
     if (c->d_partials) (void)hipFree(c->d_partials);
     c->d_partials = nullptr;
-    // two slots: the pipelined kernel has two iterations in flight
-    GQ_HIP(hipMalloc((void **)&c->d_partials, 2 * sizeof(fix128) * (size_t)c->nblocks * (NFIX + c->L) + 64));
-    if (c->d_done_it) (void)hipFree(c->d_done_it);
-    c->d_done_it = nullptr;
-    GQ_HIP(hipMalloc((void **)&c->d_done_it, sizeof(int) * (size_t)c->nblocks));
+    GQ_HIP(hipMalloc((void **)&c->d_partials, sizeof(fix128) * (size_t)c->nblocks * (NFIX + c->L) + 64));
     return GQMAP_OK;
 }
 
@@ -1253,8 +1022,7 @@ FinParams fin_params(const gqmap_ctx *c)
 }
 
 // Resident workgroups per CU for a k_iter instantiation, and CUs per XCD:
-// the tile grouping of k_iter (speed only, never results), and the grid of
-// the pipelined kernel (one workgroup per resident slot).
+// the tile grouping of k_iter (speed only, never results).
 template <typename K>
 int2 kernel_shape(K kern)
 {
@@ -1278,8 +1046,8 @@ struct TileSegs {
 // [0, bnd) and [bnd, nblocks).
 void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
 {
-    const int TM = c->split == 1 ? 16 : c->split == 4 ? 8 : 4;
-    const int tm = c->tiles_m, cb0 = c->own_lo / TM, cb1 = (c->own_hi - 1) / TM;
+    const int TN = BLOCK / c->split / tile_rows(c->split);  // tile columns
+    const int tm = c->tiles_m, cb0 = c->own_lo / TN, cb1 = (c->own_hi - 1) / TN;
     bnd.lo[0] = cb0 * tm; bnd.n[0] = tm;
     bnd.lo[1] = cb1 * tm; bnd.n[1] = cb1 != cb0 ? tm : 0;
     bnd.part_off = 0;
@@ -1290,7 +1058,7 @@ void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
 }
 
 template <typename R, typename VT, int ENG, int Q>
-void launch_k_iter(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
+void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
 {
     IterParams<R, VT> P = iter_params<R, VT>(c);
     int nblocks = c->nblocks;
@@ -1303,15 +1071,6 @@ void launch_k_iter(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
         nblocks = (sg->n[0] + sg->n[1]) * c->lpar;
         if (nblocks == 0) return;
     }
-    if (pipe_n > 0) {
-        static const int2 shp = kernel_shape(k_iter_pipe<R, VT, ENG, Q>);
-        const int nb = c->nblocks;
-        k_pipe_prep<<<(nb + 255) / 256, 256, 0, c->stream>>>(c->d_ctl, c->d_done_it, nb);
-        // block 0 is the finalizer, the others take items
-        const int grid = (int)std::max<int64_t>(2, std::min<int64_t>((int64_t)shp.x * shp.y, (int64_t)nb * pipe_n + 1));
-        k_iter_pipe<R, VT, ENG, Q><<<grid, BLOCK, 0, c->stream>>>(P, pipe_n, c->d_done_it);
-        return;
-    }
     static const int2 shape = kernel_shape(k_iter<R, VT, ENG, Q>);
     if (!getenv("GQMAP_NO_CU_GROUP")) {
         P.cu_group = shape.x;
@@ -1323,47 +1082,36 @@ void launch_k_iter(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
 }
 
 template <typename R, typename VT, int ENG>
-void launch_iter_q(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
+void launch_iter_q(gqmap_ctx *c, const TileSegs *sg)
 {
     if (c->split == 16)
-        launch_k_iter<R, VT, ENG, 16>(c, pipe_n, sg);
+        launch_k_iter<R, VT, ENG, 16>(c, sg);
     else if (c->split == 4)
-        launch_k_iter<R, VT, ENG, 4>(c, pipe_n, sg);
+        launch_k_iter<R, VT, ENG, 4>(c, sg);
+    else if (c->split == 2)
+        launch_k_iter<R, VT, ENG, 2>(c, sg);
     else
-        launch_k_iter<R, VT, ENG, 1>(c, pipe_n, sg);
+        launch_k_iter<R, VT, ENG, 1>(c, sg);
 }
 
 template <typename R, typename VT>
-void launch_iter_t(gqmap_ctx *c, int pipe_n, const TileSegs *sg)
+void launch_iter_t(gqmap_ctx *c, const TileSegs *sg)
 {
     switch (c->opt.engine) {
-    case GQMAP_ENGINE_SUPER: launch_iter_q<R, VT, 1>(c, pipe_n, sg); break;
-    case GQMAP_ENGINE_CTF: launch_iter_q<R, VT, 2>(c, pipe_n, sg); break;
-    default: launch_iter_q<R, VT, 0>(c, pipe_n, sg); break;
+    case GQMAP_ENGINE_SUPER: launch_iter_q<R, VT, 1>(c, sg); break;
+    case GQMAP_ENGINE_CTF: launch_iter_q<R, VT, 2>(c, sg); break;
+    default: launch_iter_q<R, VT, 0>(c, sg); break;
     }
 }
 
-// pipe_n > 0: one pipelined launch (k_iter_pipe) of pipe_n iterations;
 // sg: a subset of the tiles (default: all, one launch)
-void launch_iter(gqmap_ctx *c, int pipe_n = 0, const TileSegs *sg = nullptr)
+void launch_iter(gqmap_ctx *c, const TileSegs *sg = nullptr)
 {
-    if (c->fp32) launch_iter_t<float, float>(c, pipe_n, sg);
-    else if (c->vv32) launch_iter_t<double, vvs_t>(c, pipe_n, sg);
-    else launch_iter_t<double, double>(c, pipe_n, sg);
+    if (c->fp32) launch_iter_t<float, float>(c, sg);
+    else if (c->vv32) launch_iter_t<double, vvs_t>(c, sg);
+    else launch_iter_t<double, double>(c, sg);
 }
 
-// The pipelined kernel applies when nothing an item reads changes between
-// iterations: one Gaussian (no alpha update), constant temperature, a single
-// context (tiles exchange ghosts between launches).  Opt-in (GQMAP_PIPE=1):
-// bit-identical, but on the C2 frame its dynamically dealt tiles lose the L1
-// sharing of co-resident neighbour tiles and run ~1.5x longer each, which
-// costs more than the fill/drain it saves (profiles/r01_kernel_experiments.txt).
-bool use_pipe(const gqmap_ctx *c)
-{
-    const char *e = std::getenv("GQMAP_PIPE");
-    return e && *e == '1' && fused_finalize(c) && c->n_tiles == 1 && c->L == 1 && c->opt.t_decay_every <= 0;
-}
-constexpr int PIPE_CHUNK = 500;  // iterations per pipelined launch
 
 void launch_finalize(gqmap_ctx *c) { k_finalize<<<1, 256, 0, c->stream>>>(fin_params(c)); }
 
@@ -1480,7 +1228,7 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     TileSegs bnd, inr;
     tile_segments(c, bnd, inr);
     if (e0) GQ_HIP(hipEventRecord(e0, c->stream));
-    launch_iter(c, 0, &bnd);
+    launch_iter(c, &bnd);
     GQ_HIP(hipEventRecord(c->ev_bnd, c->stream));
     GQ_HIP(hipStreamWaitEvent(c->side, c->ev_bnd, 0));
     halo_pack(c, c->side);
@@ -1494,7 +1242,7 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
         GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->side));
     }
     GQ_NCCL(R->GroupEnd());
-    launch_iter(c, 0, &inr);
+    launch_iter(c, &inr);
     if (e1) GQ_HIP(hipEventRecord(e1, c->stream));
     k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)r * NP,
                                              c->d_ctl);
@@ -2059,9 +1807,7 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         const int chunk = std::min(n_iter - total, TRACE_CAP);
         int left = chunk;
         static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
-        if (use_pipe(c)) {
-            for (; left > 0; left -= std::min(left, PIPE_CHUNK)) launch_iter(c, std::min(left, PIPE_CHUNK));
-        } else if (left >= GRAPH_CHUNK && !no_graph) {
+        if (left >= GRAPH_CHUNK && !no_graph) {
             if ((s = ensure_graph(c)) != GQMAP_OK) return s;
             while (left >= GRAPH_CHUNK) {
                 GQ_HIP(hipGraphLaunch(c->graph, c->stream));
@@ -2101,24 +1847,15 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     std::vector<hipEvent_t> ev((size_t)2 * n_iter + 2);
     for (auto &e : ev) GQ_HIP(hipEventCreate(&e));
     GQ_HIP(hipEventRecord(ev[0], c->stream));
-    const bool pipe = use_pipe(c);
-    for (int i = 0; i < n_iter;) {
-        // pipelined: one launch covers up to PIPE_CHUNK iterations, timed as a whole
-        const int n = pipe ? std::min(n_iter - i, PIPE_CHUNK) : 1;
+    for (int i = 0; i < n_iter; ++i) {
         if (c->comm) {  // both k_iter launches (boundary, interior) of the iteration
             if ((s = launch_step_rccl(c, ev[2 + 2 * i], ev[3 + 2 * i])) != GQMAP_OK) return s;
-            i += 1;
             continue;
         }
         GQ_HIP(hipEventRecord(ev[2 + 2 * i], c->stream));
-        launch_iter(c, pipe ? n : 0);
+        launch_iter(c);
         GQ_HIP(hipEventRecord(ev[3 + 2 * i], c->stream));
-        if (!pipe && (s = launch_tail(c)) != GQMAP_OK) return s;
-        for (int k = 1; k < n; ++k) {  // empty intervals for the other iterations of the launch
-            GQ_HIP(hipEventRecord(ev[2 + 2 * (i + k)], c->stream));
-            GQ_HIP(hipEventRecord(ev[3 + 2 * (i + k)], c->stream));
-        }
-        i += n;
+        if ((s = launch_tail(c)) != GQMAP_OK) return s;
     }
     GQ_HIP(hipEventRecord(ev[1], c->stream));
     GQ_HIP(hipEventSynchronize(ev[1]));
@@ -2134,9 +1871,6 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     for (auto &e : ev) (void)hipEventDestroy(e);
     Ctl h;
     if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
-    if (pipe && GQ_PIPE_STATS)
-        fprintf(stderr, "pipe stats (last launch): items %llu, wait %.3g Mcycles, busy %.3g Mcycles (wait %.1f%%)\n",
-                h.st_items, h.st_wait / 1e6, h.st_busy / 1e6, 100.0 * h.st_wait / (h.st_wait + h.st_busy + 1e-9));
     if (n_done) *n_done = h.it - h0.it;
     if (total_ms) *total_ms = t;
     if (iter_kernel_ms) *iter_kernel_ms = sum;
@@ -2515,7 +2249,7 @@ void gqmap_destroy(gqmap_ctx *c)
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace,
-                    (void *)c->d_done_it, c->d_truth};
+                    c->d_truth};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

@@ -80,7 +80,7 @@ typedef struct gqmap_options {
     double sig_lo, sig_hi;  /* 0.01 / 23 mixture (:43-44), 0.01 / 25 super       */
     double corr_tor;     /* 1-1e-5 (:7)                                          */
     double tor;          /* 1e-4 stop threshold on ptdmu (:25,75)                */
-    int split;           /* lanes per node Q (1/4/16), 0 = auto from the grid size;
+    int split;           /* lanes per node Q (1/2/4/16), 0 = auto from the grid size;
                             part of the arithmetic (partial quadrature sums)    */
     double sig_step;     /* sigma step scale: 1, ctf 0.3 (gqmap_ctf.m:34-35)     */
     double sig_init;     /* init sigma = U + sig_init; < 0: U + (max - min)      */

@@ -16,6 +16,8 @@ if engine == "super":
     o.update(temperature=0.2, drate=0.75, lambdas=16.0)
 else:
     I1, I2, flo, unk, o = setup_problem("rubberwhale", 1, 9)
+if os.environ.get("GQMAP_SPLIT"):
+    o["split"] = int(os.environ["GQMAP_SPLIT"])
 with Engine(o, I1, I2, engine, prec) as eng:
     eng.init_state(0)
     done, tot, ker = eng.run_timed(its)

@@ -254,16 +254,17 @@ def _run_engine(o, I1, I2, engine, precision, st, its):
 
 @pytest.mark.parametrize("precision", ["fp64", "fp32"])
 @pytest.mark.parametrize("engine,K,M,N,split", [("mixture", 9, 96, 128, 1),
+                                                ("mixture", 9, 96, 128, 2),
                                                 ("mixture", 9, 70, 90, 4),
                                                 ("super", 11, 96, 128, 16),
                                                 ("super", 11, 100, 132, 1),
                                                 ("ctf", 11, 96, 128, 1),
+                                                ("ctf", 11, 96, 128, 2),
                                                 ("ctf", 11, 60, 70, 4),
                                                 ("ctf", 11, 30, 44, 16)])
-def test_pipelined_kernel_bit_exact_vs_emulator(engine, K, M, N, split, precision, monkeypatch):
-    # L = 1, constant temperature: the pipelined kernel (opt-in GQMAP_PIPE=1;
-    # iterations overlap across tiles, one launch per chunk) against the CPU model
-    monkeypatch.setenv("GQMAP_PIPE", "1")
+def test_single_gaussian_every_split_bit_exact_vs_emulator(engine, K, M, N, split, precision):
+    # L = 1, constant temperature, every lanes-per-node Q (16 x 16, 16 x 8,
+    # 8 x 8, 4 x 4 node tiles) against the CPU model
     I1, I2, _, _, o, st = _reference_init_case("rubberwhale", M, N, 150, 200, L=1, K=K, engine=engine,
                                                split=split, t_decay_every=0)
     e_done, e_tr, e_T, ost = _emulate(o, I1, I2, st, 40, precision, split)
@@ -272,13 +273,12 @@ def test_pipelined_kernel_bit_exact_vs_emulator(engine, K, M, N, split, precisio
     _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
 
 
-def test_pipelined_equals_per_iteration_launches(monkeypatch):
-    # full C2 frame, 120 iterations: one pipelined launch against 2 graph
-    # chunks of 50 + 20 single launches
+def test_graph_replay_equals_per_iteration_launches(monkeypatch):
+    # full C2 frame, 120 iterations: 2 captured 50-iteration graphs + 20
+    # single launches against 120 single launches (GQMAP_NO_GRAPH)
     I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 388, 584)
-    monkeypatch.setenv("GQMAP_PIPE", "1")
     a = _run_engine(o, I1, I2, "mixture", "fp64", st, 120)
-    monkeypatch.delenv("GQMAP_PIPE")
+    monkeypatch.setenv("GQMAP_NO_GRAPH", "1")
     b = _run_engine(o, I1, I2, "mixture", "fp64", st, 120)
     assert a[0] == b[0] == 120
     np.testing.assert_array_equal(a[1], b[1])
@@ -286,17 +286,17 @@ def test_pipelined_equals_per_iteration_launches(monkeypatch):
         np.testing.assert_array_equal(getattr(a[2], k), getattr(b[2], k), err_msg=k)
 
 
-def test_pipelined_stop_mid_run(monkeypatch):
-    # stop rule inside a pipelined launch: iteration s+1 runs speculatively
-    # and is discarded; the state, trace and counters equal the per-iteration
-    # path's, and later launches are no-ops
+def test_stop_inside_a_graph_chunk():
+    # the stop rule (ptdmu < tor, gqmap_gpu_mixture.m:75) firing inside a
+    # replayed 50-iteration graph: the remaining launches are no-ops, the
+    # state is that of the stopping iteration, later runs do nothing
     I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 96, 128, 150, 200)
     _, tr, _, _ = _run_engine(o, I1, I2, "mixture", "fp64", st, 60)
     ptd = tr[:, 1]
-    k = int(np.argmin(ptd))  # the first iteration with ptdmu < tor is then row k
+    k = int(np.argmin(ptd[:45]))  # stop at row k (< 50: inside the first graph chunk)
     o = dict(o, tor=float(ptd[k]) * (1 + 1e-12))
-    ref = _run_engine(o, I1, I2, "mixture", "fp64", st, 60)
-    monkeypatch.setenv("GQMAP_PIPE", "1")
+    if np.any(ptd[:k] < o["tor"]):
+        k = int(np.argmax(ptd < o["tor"]))
     from gqmap_opticalflow_amd import Engine
     with Engine(o, I1, I2) as eng:
         eng.set_state(st)
@@ -305,11 +305,12 @@ def test_pipelined_stop_mid_run(monkeypatch):
         assert eng.info().stopped == 1
         assert eng.run(30)[0] == 0
         np.testing.assert_array_equal(eng.get_state().muu, g.muu)
-    assert done == ref[0] == k + 1
-    np.testing.assert_array_equal(tr2, ref[1])
+    assert done == k + 1
+    np.testing.assert_array_equal(tr2, tr[:k + 1])
+    ref = _run_engine(o, I1, I2, "mixture", "fp64", st, k + 1)
     for key in G.STATE_KEYS:
         np.testing.assert_array_equal(getattr(g, key), getattr(ref[2], key), err_msg=key)
-    assert g.it == ref[2].it
+    assert g.it == ref[2].it == k + 2
 
 
 def test_device_math_matches_host():
