@@ -85,6 +85,9 @@ __device__ __forceinline__ float gq_sqrt_dev(float x)
 #ifndef GQ_FIN_GROUP
 #define GQ_FIN_GROUP 1  // finalize: the NFIX fixed sums loaded together (fp32 C2 -2 us)
 #endif
+#ifndef GQ_EDGE_PK  // fp32: mirror-pair edge sums on packed float2 registers (bit-identical)
+#define GQ_EDGE_PK 1
+#endif
 #ifndef GQ_TAB_LDS
 #define GQ_TAB_LDS 1
 #endif
@@ -213,6 +216,65 @@ __device__ __forceinline__ bool finite_d(double x) { return (bits_of(x) & 0x7ff0
 
 __device__ __forceinline__ double shfl_xor_r(double v, int o) { return __shfl_xor(v, o, 64); }
 __device__ __forceinline__ float shfl_xor_r(float v, int o) { return __shfl_xor(v, o, 64); }
+
+// ---------------------------------------------------------------------------
+// fp32 edge sums on packed registers.  A mirror pair's two potentials (d =
+// C +- p) travel as one float2 through v_pk_add_f32 / v_pk_fma_f32, and the
+// six accumulators as three float2 against adjacent table rows (W, WA),
+// (WXI, WXJ), (WM, WX).  Every lane of a packed op is the scalar op of
+// gqmap_math.h edge_sums in the same order: bit-identical to it (and to the
+// CPU model, which runs the scalar form).
+// ---------------------------------------------------------------------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
+// gq_sqrt_dev(float) of both lanes: v_sqrt_f32 each, the neighbour residuals packed
+__device__ __forceinline__ f2v sqrt2_pk(f2v x)
+{
+    const f2v s = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+    const f2v sm = {__int_as_float(__float_as_int(s.x) - 1), __int_as_float(__float_as_int(s.y) - 1)};
+    const f2v sp = {__int_as_float(__float_as_int(s.x) + 1), __int_as_float(__float_as_int(s.y) + 1)};
+    const f2v rm = pk_fma(-sm, s, x), rp = pk_fma(-sp, s, x);
+    f2v r;
+    r.x = rp.x > 0.f ? sp.x : (rm.x <= 0.f ? sm.x : s.x);
+    r.y = rp.y > 0.f ? sp.y : (rm.y <= 0.f ? sm.y : s.y);
+    return r;
+}
+
+template <typename TP>
+__device__ __forceinline__ Sums<float> edge_sums_pk(TP tab, int k0, int K2, int dk, float eps, const EdgeCoef<float> &c)
+{
+    f2v s0a = {0.f, 0.f}, sij = {0.f, 0.f}, smx = {0.f, 0.f};  // (s0, sa), (sxi, sxj), (sm, sx)
+    const int np = K2 >> 1;
+    GQ_PAIR_UNROLL
+    for (int k = k0; k < np; k += dk) {
+        const float p = fma(c.A, tab[tab_at(T_XI, k)], c.B * tab[tab_at(T_XJ, k)]);
+        const f2v d = f2v{c.C, c.C} + f2v{p, -p};  // C + p, C - p
+        const f2v f = sqrt2_pk(pk_fma(d, d, f2v{eps, eps}));
+        const f2v fs = f2v{f.x, f.x} + f2v{f.y, f.y}, fd = f2v{f.x, f.x} - f2v{f.y, f.y};
+        s0a = pk_fma(f2v{tab[tab_at(T_W, k)], tab[tab_at(T_WA, k)]}, fs, s0a);
+        sij = pk_fma(f2v{tab[tab_at(T_WXI, k)], tab[tab_at(T_WXJ, k)]}, fd, sij);
+        smx = pk_fma(f2v{tab[tab_at(T_WM, k)], tab[tab_at(T_WX, k)]}, fs, smx);
+    }
+    Sums<float> S;
+    S.s0 = s0a.x; S.sa = s0a.y; S.sxi = sij.x; S.sxj = sij.y; S.sm = smx.x; S.sx = smx.y;
+    if ((K2 & 1) && np >= k0 && (np - k0) % dk == 0) {  // the centre point (xi = xj = 0)
+        const int k = np;
+        const float d = fma(c.A, tab[tab_at(T_XI, k)], fma(c.B, tab[tab_at(T_XJ, k)], c.C));
+        S.add(tab, k, gq_sqrt_dev(fma(d, d, eps)));
+    }
+    return S;
+}
+
+template <typename R, typename TP>
+__device__ __forceinline__ Sums<R> edge_sums_dev(TP tab, int k0, int K2, int dk, R eps, const EdgeCoef<R> &c)
+{
+    if constexpr (sizeof(R) == 4 && GQ_EDGE_PK)
+        return edge_sums_pk(tab, k0, K2, dk, eps, c);
+    else
+        return edge_sums(tab, k0, K2, dk, eps, c);
+}
 
 // Combine the Q partial quadrature sums of a node's lane group (adjacent
 // lanes): the xor butterfly of gqmap_math.h's butterfly(), every lane ends
@@ -533,7 +595,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                 const R p = src[h + MNL * (5 + dir + 2 * uv)];  // rou plane 5+e
                 const R o2 = src[r + MNL * (2 + uv)];
                 const EdgeCoef<R> c = edge_coef(u1, src[r + MNL * uv], o1, o2, p);
-                Sums<R> S = edge_sums(tab, kj, K2, Q, P.epsn, c);
+                Sums<R> S = edge_sums_dev(tab, kj, K2, Q, P.epsn, c);
                 if (Q > 1) S = lane_combine<Q>(S);
                 g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p, ENG == 2);
                 // the edge owns its correlation: clamped ascent right here
@@ -988,7 +1050,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.sig_lo = R(o.sig_lo); P.sig_hi = R(o.sig_hi); P.corr = R(o.corr_tor);
     P.sig_step = R(o.sig_step);
     double xmax = 0;
-    for (int k = 0; k < c->K2; ++k) xmax = std::max(xmax, std::fabs(c->tab_host[tab_at(0, k)]));
+    for (int k = 0; k < c->K2; ++k) xmax = std::max(xmax, std::fabs(c->tab_host[tab_at(T_XI, k)]));
     P.gh_xmax = R(xmax);
     P.truth = c->d_truth;
     P.step0 = o.step0; P.step_decay = o.step_decay;
@@ -1580,14 +1642,14 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
         for (int r = 0; r < c->K; ++r) {
             const int k = r + c->K * cc;
             const double xi = X[cc], xj = X[r], w = W[cc] * W[r];
-            c->tab_host[tab_at(0, k)] = xi;
-            c->tab_host[tab_at(1, k)] = xj;
-            c->tab_host[tab_at(2, k)] = w;
-            c->tab_host[tab_at(3, k)] = w * xi;
-            c->tab_host[tab_at(4, k)] = w * xj;
-            c->tab_host[tab_at(5, k)] = w * (xi * xi + xj * xj);
-            c->tab_host[tab_at(6, k)] = w * (xi * xi - xj * xj);
-            c->tab_host[tab_at(7, k)] = w * (xi * xj);
+            c->tab_host[tab_at(T_XI, k)] = xi;
+            c->tab_host[tab_at(T_XJ, k)] = xj;
+            c->tab_host[tab_at(T_W, k)] = w;
+            c->tab_host[tab_at(T_WXI, k)] = w * xi;
+            c->tab_host[tab_at(T_WXJ, k)] = w * xj;
+            c->tab_host[tab_at(T_WA, k)] = w * (xi * xi + xj * xj);
+            c->tab_host[tab_at(T_WM, k)] = w * (xi * xi - xj * xj);
+            c->tab_host[tab_at(T_WX, k)] = w * (xi * xj);
         }
     gqmap_status st = GQMAP_OK;
     auto fail = [&](gqmap_status s) { gqmap_destroy(c); return s; };

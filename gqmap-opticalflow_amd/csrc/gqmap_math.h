@@ -34,7 +34,12 @@ namespace gq {
 #endif
 
 constexpr int TAB_STRIDE = 256;  // quadrature points the table holds (K2 <= 256)
-constexpr int NTAB = 8;          // xi, xj, w, w*xi, w*xj, w*(xi^2+xj^2), w*(xi^2-xj^2), w*xi*xj
+constexpr int NTAB = 8;          // entries per quadrature point, rows below
+// Table rows: the node XI, XJ, the weight W = WIWJ and W times the basis
+// monomials.  Rows a packed fp32 update reads as one pair are adjacent
+// ((W, W a), (W XI, W XJ), (W m, W x)).
+constexpr int T_XI = 0, T_XJ = 1, T_W = 2, T_WA = 3, T_WXI = 4, T_WXJ = 5, T_WM = 6, T_WX = 7;
+//   WA = W (XI^2 + XJ^2), WM = W (XI^2 - XJ^2), WX = W XI XJ
 // Table entry r of quadrature point k.  Point-major: the 8 entries of a
 // point are contiguous, so a wave-uniform point costs one scalar load
 // (s_load_dwordx8 / x16) instead of eight.
@@ -408,19 +413,19 @@ struct Grad {
 //   sa = sum W (XI^2+XJ^2) f, sm = sum W (XI^2-XJ^2) f, sx = sum W XI XJ f.
 // Every accumulator of the reference (dp, du1, du2, do1, do2, Ei;
 // gqmap_gpu_mixture.m:99-105) is a fixed linear combination of these six.
-// Table rows: 0 XI, 1 XJ, 2 W, 3 W XI, 4 W XJ, 5 W(XI^2+XJ^2), 6 W(XI^2-XJ^2), 7 W XI XJ.
+// Table rows: T_XI .. T_WX above.
 template <typename R>
 struct Sums {
     R s0 = 0, sxi = 0, sxj = 0, sa = 0, sm = 0, sx = 0;
     template <typename TP>
     GQ_HD void add(TP tab, int k, R f)
     {
-        s0 = fma(tab[tab_at(2, k)], f, s0);
-        sxi = fma(tab[tab_at(3, k)], f, sxi);
-        sxj = fma(tab[tab_at(4, k)], f, sxj);
-        sa = fma(tab[tab_at(5, k)], f, sa);
-        sm = fma(tab[tab_at(6, k)], f, sm);
-        sx = fma(tab[tab_at(7, k)], f, sx);
+        s0 = fma(tab[tab_at(T_W, k)], f, s0);
+        sxi = fma(tab[tab_at(T_WXI, k)], f, sxi);
+        sxj = fma(tab[tab_at(T_WXJ, k)], f, sxj);
+        sa = fma(tab[tab_at(T_WA, k)], f, sa);
+        sm = fma(tab[tab_at(T_WM, k)], f, sm);
+        sx = fma(tab[tab_at(T_WX, k)], f, sx);
     }
     // point k and its mirror K^2-1-k (xi, xj -> -xi, -xj: the Gauss-Hermite
     // rule is symmetric, so w, w(xi^2+-xj^2), w xi xj are shared and w xi,
@@ -429,12 +434,12 @@ struct Sums {
     GQ_HD void add_pair(TP tab, int k, R fp, R fm)
     {
         const R fs = fp + fm, fd = fp - fm;
-        s0 = fma(tab[tab_at(2, k)], fs, s0);
-        sxi = fma(tab[tab_at(3, k)], fd, sxi);
-        sxj = fma(tab[tab_at(4, k)], fd, sxj);
-        sa = fma(tab[tab_at(5, k)], fs, sa);
-        sm = fma(tab[tab_at(6, k)], fs, sm);
-        sx = fma(tab[tab_at(7, k)], fs, sx);
+        s0 = fma(tab[tab_at(T_W, k)], fs, s0);
+        sxi = fma(tab[tab_at(T_WXI, k)], fd, sxi);
+        sxj = fma(tab[tab_at(T_WXJ, k)], fd, sxj);
+        sa = fma(tab[tab_at(T_WA, k)], fs, sa);
+        sm = fma(tab[tab_at(T_WM, k)], fs, sm);
+        sx = fma(tab[tab_at(T_WX, k)], fs, sx);
     }
 };
 
@@ -552,12 +557,12 @@ GQ_HD Sums<R> edge_sums(TP tab, int k0, int K2, int dk, R eps, const EdgeCoef<R>
         k0, K2, dk,
         [&](int k) {
             // d = C +- p with p = A xi + B xj
-            const R p = fma(c.A, tab[tab_at(0, k)], c.B * tab[tab_at(1, k)]);
+            const R p = fma(c.A, tab[tab_at(T_XI, k)], c.B * tab[tab_at(T_XJ, k)]);
             const R dp = c.C + p, dm = c.C - p;
             S.add_pair(tab, k, GQ_SQRT(fma(dp, dp, eps)), GQ_SQRT(fma(dm, dm, eps)));
         },
         [&](int k) {
-            const R d = fma(c.A, tab[tab_at(0, k)], fma(c.B, tab[tab_at(1, k)], c.C));
+            const R d = fma(c.A, tab[tab_at(T_XI, k)], fma(c.B, tab[tab_at(T_XJ, k)], c.C));
             S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
         });
     return S;
@@ -608,8 +613,8 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
             const R U1 = u1 + R(n + 1), U2 = u2 + R(m + 1);
             GQ_NODE_UNROLL
             for (int k = k0; k < K2; k += dk) {
-                const R X = fma(c.ax, tab[tab_at(0, k)], fma(c.bx, tab[tab_at(1, k)], U1));
-                const R Y = fma(c.ay, tab[tab_at(0, k)], fma(c.by, tab[tab_at(1, k)], U2));
+                const R X = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], U1));
+                const R Y = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], U2));
                 const R d = fma(sample4_abs<CLAMP>(VV, M2, Mo, No, X, Y), R(-0.25), I);
                 S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
             }
@@ -618,8 +623,8 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
             // cells: measured slower for the gathers, unlike the edge sums)
             GQ_NODE_UNROLL
             for (int k = k0; k < K2; k += dk) {
-                const R x1 = fma(c.ax, tab[tab_at(0, k)], fma(c.bx, tab[tab_at(1, k)], u1));
-                const R x2 = fma(c.ay, tab[tab_at(0, k)], fma(c.by, tab[tab_at(1, k)], u2));
+                const R x1 = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], u1));
+                const R x2 = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], u2));
                 const R v4 = ENG == 2 ? sample_ctf4(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
                                       : sample4<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
                 const R d = fma(v4, R(-0.25), I);
@@ -633,8 +638,8 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
         for (int q = 0; q < 16; ++q) I[q] = I1[(i0 + (q >> 2)) + (int64_t)Mo * (j0 + (q & 3))];
         // (one point at a time: a pair of 4x4 block sums costs more VGPRs than it saves)
         for (int k = k0; k < K2; k += dk) {
-            const R x1 = fma(c.ax, tab[tab_at(0, k)], fma(c.bx, tab[tab_at(1, k)], u1));
-            const R x2 = fma(c.ay, tab[tab_at(0, k)], fma(c.by, tab[tab_at(1, k)], u2));
+            const R x1 = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], u1));
+            const R x2 = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], u2));
             S.add(tab, k, super_block_sum<R>(VV, M2, Mo, No, i0, j0, x1, x2, eps, I));
         }
     }

@@ -95,14 +95,14 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
         for (int r = 0; r < P->K; ++r) {
             const int k = r + P->K * cc;
             const double xi = X[cc], xj = X[r], ww = W[cc] * W[r];
-            tabd[tab_at(0, k)] = xi;
-            tabd[tab_at(1, k)] = xj;
-            tabd[tab_at(2, k)] = ww;
-            tabd[tab_at(3, k)] = ww * xi;
-            tabd[tab_at(4, k)] = ww * xj;
-            tabd[tab_at(5, k)] = ww * (xi * xi + xj * xj);
-            tabd[tab_at(6, k)] = ww * (xi * xi - xj * xj);
-            tabd[tab_at(7, k)] = ww * (xi * xj);
+            tabd[tab_at(T_XI, k)] = xi;
+            tabd[tab_at(T_XJ, k)] = xj;
+            tabd[tab_at(T_W, k)] = ww;
+            tabd[tab_at(T_WXI, k)] = ww * xi;
+            tabd[tab_at(T_WXJ, k)] = ww * xj;
+            tabd[tab_at(T_WA, k)] = ww * (xi * xi + xj * xj);
+            tabd[tab_at(T_WM, k)] = ww * (xi * xi - xj * xj);
+            tabd[tab_at(T_WX, k)] = ww * (xi * xj);
         }
     w.tab.assign(tabd.begin(), tabd.end());
     const size_t nvv = (size_t)(w.Mo + 2) * (w.No + 2), ni = (size_t)w.Mo * w.No;
