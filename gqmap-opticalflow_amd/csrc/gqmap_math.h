@@ -176,6 +176,10 @@ GQ_HD void keys4(R t, R &w0, R &w1, R &w2, R &w3)
     w3 = fma(t2, t, -t2);
 }
 
+#ifndef GQ_WAVE_ALL  // device: the predicate over the lanes of the wave; host: the lane's own
+#define GQ_WAVE_ALL(x) (x)
+#endif
+
 #ifndef GQ_UMUL24  // 24-bit multiply (full rate on the device; both factors < 2^24)
 #define GQ_UMUL24(a, b) ((uint32_t)(a) * (uint32_t)(b))
 #endif
@@ -266,6 +270,20 @@ GQ_HD void axis_cell(int j, float x, int n, int &ix, float &fr)
     if (CLAMP && ix > n - 1) { ix = n - 1; fr = 1.f; }
 }
 
+// Relative form for both precisions: integer cell + fraction of the
+// displacement x from the 1-based pixel j (the super engine's per-pixel path:
+// an unclamped sample gets exactly the cell j + floor(x) and fraction
+// x - floor(x) of the shared 7x7 window, so the two branches agree bit for bit).
+template <typename R>
+GQ_HD void axis_cell_rel(int j, R x, int n, int &ix, R &fr)
+{
+    x = fmin(fmax(x, R(1 - j)), R(n - j));
+    const R f = floor(x);
+    fr = x - f;
+    ix = j + (int)f;
+    if (ix > n - 1) { ix = n - 1; fr = R(1); }
+}
+
 // 4 x interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV.
 // CLAMP = false: the caller guarantees 1 <= jj + x1 < No and 1 <= ii + x2 < Mo
 // for this sample, where every clamp is the identity -- same result.
@@ -323,15 +341,21 @@ GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 // cell (i + floor(x2), j + floor(x1)): the 16 cells tile one 7x7 tap window,
 // so the 28 column sums are shared (49 taps instead of 256).  Each output
 // uses exactly the fma sequence of bicubic_cell.  Blocks touching the border
-// take the reference per-sample position arithmetic (sample()).
+// take per-sample clamped positions (axis_cell_rel: the reference's clamp,
+// relative to the pixel), which for an unclamped block give the same cells,
+// fractions and bits as the shared window.
 // I[q], q = 4*di + dj (j fastest, the reference loop order).
 // ---------------------------------------------------------------------------
 template <typename R, typename VP>
 GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x2, R eps,
                         const R (&I)[16])
 {
-    const bool safe = R(j0 + 1) + x1 >= R(1) && R(j0 + 4) + x1 <= R(No - 1) &&
-                      R(i0 + 1) + x2 >= R(1) && R(i0 + 4) + x2 <= R(Mo - 1);
+    // Both branches compute every output from the same cells, fractions and
+    // fma sequence, so the choice never changes a result (GQ_WAVE_ALL: the
+    // device may take the shared window only when the whole wave can --
+    // measured neutral on C4: a VALU win early in a run, a gather loss later).
+    const bool safe = GQ_WAVE_ALL(R(j0 + 1) + x1 >= R(1) && R(j0 + 4) + x1 <= R(No - 1) &&
+                                  R(i0 + 1) + x2 >= R(1) && R(i0 + 4) + x2 <= R(Mo - 1));
     R f = 0;
     if (safe) {
         const R fx = floor(x1), fy = floor(x2);
@@ -373,19 +397,28 @@ GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x
         // weights (they depend only on dj) and per-row ones computed once:
         // identical values, C4 fp64 511 -> 402 us/it.  (fp32 keeps the plain
         // loop: the hoisted form costs it a wave per SIMD, 380 -> 480 us/it.)
+        // axis_cell_rel of each column / row from one floor per axis: the
+        // pixel j's cell is j + floor(x) with fraction x - floor(x) unless it
+        // clamps (j + floor(x) <= 0 -> cell 1, fraction 0; >= n -> cell n-1,
+        // fraction 1) -- the same values, integer compares only
+        const R fx = floor(x1), fy = floor(x2);
+        const R sx = x1 - fx, sy = x2 - fy;
+        const int ifx = (int)fx, ify = (int)fy;
         R sw[4][4];
         int ixs[4];
         GQ_UNROLL_FULL
         for (int dj = 0; dj < 4; ++dj) {
-            R fr;
-            axis_cell(j0 + dj + 1, x1, No, ixs[dj], fr);
+            const int c = j0 + dj + 1 + ifx;
+            ixs[dj] = c <= 0 ? 1 : c >= No ? No - 1 : c;
+            const R fr = c <= 0 ? R(0) : c >= No ? R(1) : sx;
             keys4(fr, sw[dj][0], sw[dj][1], sw[dj][2], sw[dj][3]);
         }
         GQ_UNROLL_FULL
         for (int di = 0; di < 4; ++di) {
-            int iy;
-            R fr, t0, t1, t2, t3;
-            axis_cell(i0 + di + 1, x2, Mo, iy, fr);
+            const int r = i0 + di + 1 + ify;
+            const int iy = r <= 0 ? 1 : r >= Mo ? Mo - 1 : r;
+            const R fr = r <= 0 ? R(0) : r >= Mo ? R(1) : sy;
+            R t0, t1, t2, t3;
             keys4(fr, t0, t1, t2, t3);
             GQ_UNROLL_FULL
             for (int dj = 0; dj < 4; ++dj) {
