@@ -107,6 +107,7 @@ __device__ __forceinline__ float gq_sqrt_dev(float x)
 #define GQ_NODE_UNROLL GQ_PRAGMA_UNROLL(GQ_NODE_UNROLL_N)
 #define GQ_UNROLL_FULL _Pragma("unroll")
 #define GQ_UMUL24(a, b) __umul24((uint32_t)(a), (uint32_t)(b))
+#define GQ_FRACT(x) __builtin_amdgcn_fract(x)  // v_fract_f64
 #ifndef GQ_SUPER_WAVE_UNIFORM  // super engine: shared-window branch only when the whole wave can take it
 #define GQ_SUPER_WAVE_UNIFORM 0  // measured: wins early (VALU), loses mid-run (gather-bound): off
 #endif

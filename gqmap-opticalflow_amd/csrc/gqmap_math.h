@@ -176,6 +176,10 @@ GQ_HD void keys4(R t, R &w0, R &w1, R &w2, R &w3)
     w3 = fma(t2, t, -t2);
 }
 
+#ifndef GQ_FRACT  // x - floor(x) (exact); the device has it as one instruction
+#define GQ_FRACT(x) ((x) - floor(x))
+#endif
+
 #ifndef GQ_WAVE_ALL  // device: the predicate over the lanes of the wave; host: the lane's own
 #define GQ_WAVE_ALL(x) (x)
 #endif
@@ -249,8 +253,12 @@ GQ_HD void axis_cell_abs(double X, int n, int &ix, double &fr)
     // min(max(.,1),N) with MATLAB's NaN-ignoring max/min (IEEE maxNum/minNum)
     if (CLAMP) X = fmin(fmax(X, 1.0), (double)n);
     ix = (int)X;  // X >= 1: truncation == floor
-    if (CLAMP) ix = ix > n - 1 ? n - 1 : ix;
-    fr = X - (double)ix;
+    if (CLAMP) {
+        ix = ix > n - 1 ? n - 1 : ix;
+        fr = X - (double)ix;
+    } else {
+        fr = GQ_FRACT(X);  // X - floor(X): the same value (X >= 1, no cap)
+    }
 }
 // 1-based pixel j displaced by x (fp64: X = j + x, the reference's form).
 template <bool CLAMP = true>
