@@ -326,13 +326,24 @@ __device__ void fin_reduce(const FinParams &F, double *tot, fix128 *sh)
     const int NP = NFIX + F.L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rows = F.nranks > 0 ? F.nranks : F.nblocks;
+    auto row_val = [&](int r, int q) -> fix128 {
+        return F.nranks > 0 ? F.gathered[(int64_t)r * NP + q] : load_fix_agent(F.partials + (int64_t)r * NP + q);
+    };
 #if GQ_FIN_GROUP
-    {   // the NFIX fixed quantities together: a row's loads in flight at once
+    {   // the NFIX fixed quantities of FIN_ROWS rows per thread together: all
+        // their (device-coherent, high-latency) loads in flight at once
+        constexpr int FIN_ROWS = 4;
         fix128 v[NFIX] = {};
-        for (int r = tid; r < rows; r += 256) {
+        for (int r0 = tid; r0 < rows; r0 += FIN_ROWS * 256) {
+            fix128 x[FIN_ROWS][NFIX];
 #pragma unroll
-            for (int q = 0; q < NFIX; ++q)
-                v[q] += F.nranks > 0 ? F.gathered[(int64_t)r * NP + q] : load_fix_agent(F.partials + (int64_t)r * NP + q);
+            for (int u = 0; u < FIN_ROWS; ++u)
+#pragma unroll
+                for (int q = 0; q < NFIX; ++q) x[u][q] = r0 + u * 256 < rows ? row_val(r0 + u * 256, q) : (fix128)0;
+#pragma unroll
+            for (int u = 0; u < FIN_ROWS; ++u)
+#pragma unroll
+                for (int q = 0; q < NFIX; ++q) v[q] += x[u][q];
         }
 #pragma unroll
         for (int q = 0; q < NFIX; ++q) {
@@ -345,8 +356,12 @@ __device__ void fin_reduce(const FinParams &F, double *tot, fix128 *sh)
     for (int q = 0; q < NP; ++q) {
 #endif
         fix128 v = 0;
-        for (int r = tid; r < rows; r += 256)
-            v += F.nranks > 0 ? F.gathered[(int64_t)r * NP + q] : load_fix_agent(F.partials + (int64_t)r * NP + q);
+        for (int r0 = tid; r0 < rows; r0 += 4 * 256) {
+            fix128 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = r0 + u * 256 < rows ? row_val(r0 + u * 256, q) : (fix128)0;
+            v += (x[0] + x[1]) + (x[2] + x[3]);
+        }
         v = wave_sum_fix(v);
         if (lane == 0) sh[q * 4 + wave] = v;
     }
