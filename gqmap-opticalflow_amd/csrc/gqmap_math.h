@@ -327,12 +327,22 @@ GQ_HD R sample(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 // entry (r, c) is the same Keys interpolation at (1+(c-1)/64, 1+(r-1)/64), so
 // the lookup is sample() at the position rounded to the 1/64 grid -- the
 // 64x table (10 GB at 480x640) is never built.  Returns 4 x the entry.
+// max(round(y), 1) with MATLAB's round (half away from zero; NaN -> 1) as
+// trunc(max(y, 1/2) + 1/2): for y >= 1/2 the sum y + 1/2 is exact or rounds
+// within [2^k, 2^k + 1/2), so its truncation is floor(y + 1/2) = round(y);
+// below 1/2 both give 1.  Four instructions instead of eight, same values.
+template <typename R>
+GQ_HD R round_ge1(R y)
+{
+    return trunc(fmax(y, R(0.5)) + R(0.5));
+}
+
 template <typename VP, typename R>
 GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 {
     const R MM = R(64 * (Mo - 1) + 1), NN = R(64 * (No - 1) + 1);
-    const R ry = fmin(fmax(round((((R)ii + x2) - R(1)) * R(64) + R(1)), R(1)), MM);
-    const R rx = fmin(fmax(round((((R)jj + x1) - R(1)) * R(64) + R(1)), R(1)), NN);
+    const R ry = fmin(round_ge1((((R)ii + x2) - R(1)) * R(64) + R(1)), MM);
+    const R rx = fmin(round_ge1((((R)jj + x1) - R(1)) * R(64) + R(1)), NN);
     const R Yq = (ry - R(1)) * R(0.015625) + R(1), Xq = (rx - R(1)) * R(0.015625) + R(1);
     int ix = (int)Xq, iy = (int)Yq;  // Xq in [1, No]: truncation == floor
     ix = ix > No - 1 ? No - 1 : ix;
