@@ -1,0 +1,49 @@
+"""Exact identities the kernel arithmetic (gqmap_math.h) relies on when it
+replaces a reference expression by a cheaper one with the same values."""
+import math
+from fractions import Fraction
+
+import numpy as np
+
+
+def _matlab_round_ge1(y: float) -> float:
+    """max(round(y), 1) with MATLAB's round (half away from zero), in exact
+    rational arithmetic; NaN -> 1 (MATLAB's max ignores NaN)."""
+    if math.isnan(y):
+        return 1.0
+    r = math.floor(abs(Fraction(y)) + Fraction(1, 2))
+    return max(float(r if y >= 0 else -r), 1.0)
+
+
+def _kernel_round_ge1(y: float) -> float:
+    """gqmap_math.h round_ge1: trunc(max(y, 1/2) + 1/2) in IEEE doubles
+    (Python floats are IEEE doubles; fmax ignores NaN)."""
+    yy = 0.5 if (math.isnan(y) or y < 0.5) else y
+    return float(math.trunc(yy + 0.5))
+
+
+def test_round_ge1_identity():
+    # sample_ctf4 (legacy/gqmap_ctf.m:96): positions rounded to the 1/64 grid
+    rng = np.random.default_rng(0)
+    ys = list(rng.uniform(-200.0, 64 * 2600.0, 50000))
+    # neighbours of half-integers and of the binade edges, where y + 1/2 rounds
+    for k in range(-2, 40):
+        for base in (2.0 ** k - 0.5, 2.0 ** k - 1.5, 2.0 ** k + 0.5):
+            v_up = v_dn = base
+            for _ in range(4):
+                v_up = float(np.nextafter(v_up, np.inf))
+                v_dn = float(np.nextafter(v_dn, -np.inf))
+                ys += [v_up, v_dn]
+            ys.append(base)
+    ys += [n + 0.5 for n in range(-5, 200)] + [0.49999999999999994, 0.5, -0.5, float("nan"), -1e300]
+    bad = [y for y in ys if _matlab_round_ge1(y) != _kernel_round_ge1(y)]
+    assert not bad, bad[:5]
+
+
+def test_fract_identity():
+    # axis_cell_abs without clamps: X - (double)(int)X == X - floor(X) for X >= 1
+    rng = np.random.default_rng(1)
+    xs = np.concatenate([rng.uniform(1.0, 3000.0, 100000), np.arange(1.0, 100.0),
+                         np.nextafter(np.arange(2.0, 100.0), 0.0)])
+    for x in xs:
+        assert x - float(int(x)) == x - math.floor(x)
