@@ -337,17 +337,27 @@ GQ_HD R round_ge1(R y)
     return trunc(fmax(y, R(0.5)) + R(0.5));
 }
 
-template <typename VP, typename R>
+// CLAMP = false: the caller guarantees 1 <= jj + x1 < No - 1/64 (and the
+// same for rows; node_unclamped with CTF_MARGIN), so round(y) lies in [1, MM)
+// and no clamp or cap acts -- the same values.
+template <bool CLAMP = true, typename VP, typename R>
 GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 {
-    const R MM = R(64 * (Mo - 1) + 1), NN = R(64 * (No - 1) + 1);
-    const R ry = fmin(round_ge1((((R)ii + x2) - R(1)) * R(64) + R(1)), MM);
-    const R rx = fmin(round_ge1((((R)jj + x1) - R(1)) * R(64) + R(1)), NN);
-    const R Yq = (ry - R(1)) * R(0.015625) + R(1), Xq = (rx - R(1)) * R(0.015625) + R(1);
-    int ix = (int)Xq, iy = (int)Yq;  // Xq in [1, No]: truncation == floor
-    ix = ix > No - 1 ? No - 1 : ix;
-    iy = iy > Mo - 1 ? Mo - 1 : iy;
-    return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, Xq - (R)ix, Yq - (R)iy);
+    const R y = (((R)ii + x2) - R(1)) * R(64) + R(1), x = (((R)jj + x1) - R(1)) * R(64) + R(1);
+    if constexpr (CLAMP) {
+        const R MM = R(64 * (Mo - 1) + 1), NN = R(64 * (No - 1) + 1);
+        const R ry = fmin(round_ge1(y), MM), rx = fmin(round_ge1(x), NN);
+        const R Yq = (ry - R(1)) * R(0.015625) + R(1), Xq = (rx - R(1)) * R(0.015625) + R(1);
+        int ix = (int)Xq, iy = (int)Yq;  // Xq in [1, No]: truncation == floor
+        ix = ix > No - 1 ? No - 1 : ix;
+        iy = iy > Mo - 1 ? Mo - 1 : iy;
+        return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, Xq - (R)ix, Yq - (R)iy);
+    } else {
+        const R ry = trunc(y + R(0.5)), rx = trunc(x + R(0.5));  // y, x >= 1: round_ge1
+        const R Yq = (ry - R(1)) * R(0.015625) + R(1), Xq = (rx - R(1)) * R(0.015625) + R(1);
+        const int ix = (int)Xq, iy = (int)Yq;
+        return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, GQ_FRACT(Xq), GQ_FRACT(Yq));
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -676,7 +686,7 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
             for (int k = k0; k < K2; k += dk) {
                 const R x1 = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], u1));
                 const R x2 = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], u2));
-                const R v4 = ENG == 2 ? sample_ctf4(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
+                const R v4 = ENG == 2 ? sample_ctf4<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
                                       : sample4<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
                 const R d = fma(v4, R(-0.25), I);
                 S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
@@ -700,10 +710,13 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
 // lies where sample()'s clamps are the identity: |x1 - u1| <= (|ax|+|bx|) xmax
 // and |x2 - u2| <= (|ay|+|by|) xmax (xmax = max |Gauss-Hermite node|), with a
 // margin far above the rounding of the position arithmetic.
+// (ctf engine: extra = CTF_MARGIN, the 1/64-grid rounding of the position
+// must not reach the last column / row either)
+constexpr double CTF_MARGIN = 1.0 / 32;
 template <typename R>
-GQ_HD bool node_unclamped(const NodeCoef<R> &c, R u1, R u2, int m, int n, int Mo, int No, R xmax)
+GQ_HD bool node_unclamped(const NodeCoef<R> &c, R u1, R u2, int m, int n, int Mo, int No, R xmax, R extra = R(0))
 {
-    const R margin = sizeof(R) == 8 ? R(1e-6) : R(1e-2);
+    const R margin = (sizeof(R) == 8 ? R(1e-6) : R(1e-2)) + extra;
     const R rx = (fabs(c.ax) + fabs(c.bx)) * xmax + margin, ry = (fabs(c.ay) + fabs(c.by)) * xmax + margin;
     // positions relative to the 1-based pixel (n+1, m+1)
     return u1 - rx >= R(-n) && u1 + rx < R(No - 1 - n) && u2 - ry >= R(-m) && u2 + ry < R(Mo - 1 - m);
