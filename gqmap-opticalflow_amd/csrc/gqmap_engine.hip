@@ -144,7 +144,7 @@ struct Ctl {
 };
 
 struct FinParams {
-    const fix128 *partials;
+    const fix128 *partials;  // q-major block partials, row stride nblocks (part_word)
     int nblocks, L;
     const fix128 *gathered;  // nranks > 0: per-tile totals [nranks][NFIX+L] (exact, any order)
     int nranks;
@@ -167,7 +167,7 @@ struct IterParams {
     R *st1;
     const R *__restrict__ tab;  // TS x NTAB, point-major (tab_at)
     Ctl *ctl;
-    fix128 *partials;           // nblocks x (NFIX + L)
+    fix128 *partials;           // (NFIX + L) x nblocks, q-major (part_word)
     int M, N, Mo, No, M2, L, K2;
     // column-strip tiling (multi-GPU): local node column n is global column
     // n + n_off of Ng; only local columns [own_lo, own_hi) are updated, the
@@ -301,19 +301,28 @@ __device__ __forceinline__ Sums<R> lane_combine(Sums<R> S)
     return S;
 }
 
-// Device-coherent 128-bit stores/loads of the block partials (two agent-scope
-// relaxed 64-bit atomics each: they bypass the non-coherent per-XCD L2s).
-__device__ __forceinline__ void store_fix_agent(fix128 *p, fix128 v)
+// Block partials, q-major: the low / high 64-bit halves of row r's quantity q
+// are words (2q) * PS + r and (2q + 1) * PS + r, PS = rows allocated (the
+// context's nblocks).  The finalize's loads of consecutive rows are then
+// contiguous: with row-major rows every lane's load touched its own cache
+// line (C2: ~10k line requests, 4 us of an 8 us reduction).
+__device__ __forceinline__ int64_t part_word(int PS, int r, int q, int half)
 {
-    uint64_t *q = reinterpret_cast<uint64_t *>(p);
-    __hip_atomic_store(q, (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, (uint64_t)(v >> 64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (int64_t)(2 * q + half) * PS + r;
 }
-__device__ __forceinline__ fix128 load_fix_agent(const fix128 *p)
+// Device-coherent stores/loads of a partial (agent-scope relaxed 64-bit
+// atomics: they bypass the non-coherent per-XCD L2s).
+__device__ __forceinline__ void store_part_agent(fix128 *parts, int PS, int r, int q, fix128 v)
 {
-    const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
-    const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t *w = reinterpret_cast<uint64_t *>(parts);
+    __hip_atomic_store(w + part_word(PS, r, q, 0), (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w + part_word(PS, r, q, 1), (uint64_t)(v >> 64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ fix128 load_part_agent(const fix128 *parts, int PS, int r, int q)
+{
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(parts);
+    const uint64_t lo = __hip_atomic_load(w + part_word(PS, r, q, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t hi = __hip_atomic_load(w + part_word(PS, r, q, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (fix128)(((unsigned __int128)hi << 64) | lo);
 }
 
@@ -323,11 +332,13 @@ __device__ void fin_reduce(const FinParams &F, double *tot, fix128 *sh)
 {
     // the NFIX fixed sums together, the dalpha sums one at a time (few live
     // registers: this code shares the k_iter register budget when fused)
-    const int NP = NFIX + F.L;
+    // (L = 1: no dalpha sum, fin_apply reads it only when L > 1)
+    const int NP = NFIX + F.L, NPR = F.L > 1 ? NP : NFIX;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rows = F.nranks > 0 ? F.nranks : F.nblocks;
+    const bool gathered = F.nranks > 0;
     auto row_val = [&](int r, int q) -> fix128 {
-        return F.nranks > 0 ? F.gathered[(int64_t)r * NP + q] : load_fix_agent(F.partials + (int64_t)r * NP + q);
+        return gathered ? F.gathered[(int64_t)r * NP + q] : load_part_agent(F.partials, F.nblocks, r, q);
     };
 #if GQ_FIN_GROUP
     {   // the NFIX fixed quantities of FIN_ROWS rows per thread together: all
@@ -351,9 +362,9 @@ __device__ void fin_reduce(const FinParams &F, double *tot, fix128 *sh)
             if (lane == 0) sh[q * 4 + wave] = w;
         }
     }
-    for (int q = NFIX; q < NP; ++q) {
+    for (int q = NFIX; q < NPR; ++q) {
 #else
-    for (int q = 0; q < NP; ++q) {
+    for (int q = 0; q < NPR; ++q) {
 #endif
         fix128 v = 0;
         for (int r0 = tid; r0 < rows; r0 += 4 * 256) {
@@ -366,7 +377,7 @@ __device__ void fin_reduce(const FinParams &F, double *tot, fix128 *sh)
         if (lane == 0) sh[q * 4 + wave] = v;
     }
     __syncthreads();
-    if (tid < NP) tot[tid] = from_fix((sh[tid * 4] + sh[tid * 4 + 1]) + (sh[tid * 4 + 2] + sh[tid * 4 + 3]));
+    if (tid < NPR) tot[tid] = from_fix((sh[tid * 4] + sh[tid * 4 + 1]) + (sh[tid * 4 + 2] + sh[tid * 4 + 3]));
     __syncthreads();
 }
 
@@ -491,12 +502,33 @@ struct TileLds {
     R tab[TPIX < BLOCK && GQ_TAB_LDS ? NTAB * TS : 1];
 };
 
+#ifndef GQ_TIMELINE
+#define GQ_TIMELINE 0
+#endif
+#if GQ_TIMELINE
+// debug builds: per-block stamps (s_memrealtime, 100 MHz) of k_iter
+// iterations GQ_TIMELINE and GQ_TIMELINE + 1 (gqmap_debug_timeline), 16 words
+// per block and iteration: 0 start, 1 wave 0 done with phase 0, 2 both
+// phases done (all waves), 3 components done, 4 partials stored, 5 HW_ID,
+// 6 XCC_ID, 7 finalize done; last block only: 8 ticket taken, 9 partials
+// reduced
+__device__ unsigned long long g_timeline[8192 * 32];
+#define TL_STAMP(s, v)                                                                        \
+    do {                                                                                      \
+        const int d_ = ctl->it - GQ_TIMELINE;                                                 \
+        if (threadIdx.x == 0 && (d_ == 0 || d_ == 1) && blockIdx.x < 8192)                    \
+            g_timeline[32 * blockIdx.x + 16 * d_ + (s)] = (v);                                 \
+    } while (0)
+#else
+#define TL_STAMP(s, v) do {} while (0)
+#endif
+
 // One tile of one iteration (absolute iteration `it`, reading state buffer
 // `parity`): node and edge gradients, neighbour scatter, clamped ascent into
-// the other buffer, and the tile's exact partial sums into part_row[0..NP).
+// the other buffer, and the tile's exact partial sums into partial row part_r.
 template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
-                                          fix128 *part_row, TileLds<R, BLOCK / Q> &lds, int l0, int l1)
+                                          int part_r, TileLds<R, BLOCK / Q> &lds, int l0, int l1)
 {
     constexpr int TPIX = BLOCK / Q;                   // nodes per tile
     constexpr int TM = tile_rows(Q), TN = TPIX / TM;  // tile rows x columns
@@ -641,8 +673,10 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             }
         }
         }
+        if (ph == 0) TL_STAMP(1, __builtin_amdgcn_s_memrealtime());
         }
         __syncthreads();
+        TL_STAMP(2, __builtin_amdgcn_s_memrealtime());
         fix128 fda = 0;
         if (inner && lead) {
             // dmuu = dmuu + sum(dmu1(:,:,:,:,1),4) + circshift(dmu2(..1,1),1) + circshift(dmu2(..2,1),1,2)
@@ -683,6 +717,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         __syncthreads();  // LDS reuse by the next component
     }
 
+    TL_STAMP(3, __builtin_amdgcn_s_memrealtime());
     // block partials: Energy, sum|dmu_u|, sum|dsigma_u|, #nonfinite, dalpha[0..L-1]
     fE = wave_sum_fix(fE);
     fmu = wave_sum_fix(fmu);
@@ -703,18 +738,10 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         const int lq = tid - NFIX;  // dalpha of the components this block ran
         if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1))
             v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        store_fix_agent(&part_row[tid], v);
+        store_part_agent(P.partials, P.fin.nblocks, part_r, tid, v);
     }
 }
 
-#ifndef GQ_TIMELINE
-#define GQ_TIMELINE 0
-#endif
-#if GQ_TIMELINE
-// debug builds: per-block start / end (s_memrealtime, 100 MHz), HW_ID and
-// XCC_ID of k_iter iteration GQ_TIMELINE (gqmap_debug_timeline)
-__device__ unsigned long long g_timeline[8192 * 4];
-#endif
 
 template <typename R, typename VT, int ENG, int Q>
 __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT> P)
@@ -735,22 +762,19 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
     // XCD (see tile_of_block): alternate the phase order among them.  Not
     // for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
     const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
-    const int NP = NFIX + P.L;
     __shared__ TileLds<R, BLOCK / Q> lds;
-    fix128 *part_row = P.partials + (int64_t)(P.part_off + b) * NP;
+    const int part_r = P.part_off + b;
     if (edge_first)
-        iter_tile<R, VT, ENG, Q, true>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, true>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1);
     else
-        iter_tile<R, VT, ENG, Q, false>(P, tile, ctl->it, ctl->done & 1, part_row, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, false>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1);
 #if GQ_TIMELINE
     __syncthreads();
-    if (threadIdx.x == 0 && ctl->it == GQ_TIMELINE && b < 8192) {
-        const unsigned long long tl1 = __builtin_amdgcn_s_memrealtime();
-        g_timeline[4 * b + 0] = tl0;
-        g_timeline[4 * b + 1] = tl1;
-        g_timeline[4 * b + 2] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-        g_timeline[4 * b + 3] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
-    }
+    TL_STAMP(0, tl0);
+    TL_STAMP(4, __builtin_amdgcn_s_memrealtime());
+    TL_STAMP(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));
+    TL_STAMP(6, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
+    const int tl_it = ctl->it;
 #endif
     if (!P.fused) return;
     const int tid = threadIdx.x;
@@ -768,12 +792,23 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
     }
     __syncthreads();
     if (!last) return;
+#if GQ_TIMELINE
+    const bool tl_on = (tl_it == GQ_TIMELINE || tl_it == GQ_TIMELINE + 1) && b < 8192 && tid == 0;
+    unsigned long long *tl_row = g_timeline + 32 * b + 16 * (tl_it - GQ_TIMELINE);
+    if (tl_on) tl_row[8] = __builtin_amdgcn_s_memrealtime();
+#endif
     __shared__ double tot[NFIX + GQMAP_LMAX];
     __shared__ fix128 sh_red[256];
     fin_reduce(P.fin, tot, sh_red);
+#if GQ_TIMELINE
+    if (tl_on) tl_row[9] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (tid == 0) {
         fin_apply(P.fin, tot);
         ctl->arrive = 0;
+#if GQ_TIMELINE
+        if (tl_on) tl_row[7] = __builtin_amdgcn_s_memrealtime();
+#endif
     }
 }
 
@@ -796,7 +831,10 @@ __global__ __launch_bounds__(256) void k_reduce_local(const fix128 *partials, in
     const int tid = threadIdx.x;
     for (int q = 0; q < NP; ++q) {
         fix128 v = 0;
-        for (int b = tid; b < nblocks; b += 256) v += partials[(int64_t)b * NP + q];
+        for (int b = tid; b < nblocks; b += 256) {
+            const uint64_t *w = reinterpret_cast<const uint64_t *>(partials);
+            v += (fix128)(((unsigned __int128)w[part_word(nblocks, b, q, 1)] << 64) | w[part_word(nblocks, b, q, 0)]);
+        }
         sh[tid] = v;
         __syncthreads();
         for (int st = 128; st > 0; st >>= 1) {
@@ -1542,7 +1580,7 @@ int gqmap_abi_version(void) { return GQMAP_ABI_VERSION; }
 // debug builds only (not in include/gqmap.h): copy the k_iter timeline
 int gqmap_debug_timeline(unsigned long long *out, int n)
 {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gq::g_timeline), sizeof(unsigned long long) * 4 * (size_t)n) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(gq::g_timeline), sizeof(unsigned long long) * 32 * (size_t)n) ==
                    hipSuccess ? 0 : -1;
 }
 #endif
