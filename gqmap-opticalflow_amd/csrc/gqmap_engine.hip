@@ -523,6 +523,64 @@ __device__ unsigned long long g_timeline[8192 * 32];
 #define TL_STAMP(s, v) do {} while (0)
 #endif
 
+// Interior node (updated by this context): rows 1..M-2, owned local columns,
+// global columns 1..Ng-2.
+template <typename R, typename VT>
+__device__ __forceinline__ bool node_interior(const IterParams<R, VT> &P, int mm, int nn)
+{
+    return mm >= 1 && mm <= P.M - 2 && nn >= P.own_lo && nn < P.own_hi && nn + P.n_off >= 1 &&
+           nn + P.n_off <= P.Ng - 2;
+}
+
+// Edge job e of a lane: e = dir + 2*uv (< 4) is the node's own down / right
+// edge, e = 4 the halo edge entering the tile (top row / left column) that
+// the lane group tid / Q computes; with its operands loaded (rou plane 5+e of
+// the head node, the tail node's mean / sigma).
+template <typename R>
+struct EdgeJob {
+    int dir, uv, hr;
+    bool need;
+    R u1, o1, p, o2, u2;
+};
+template <typename R, typename VT, int Q, int TM, int TN>
+__device__ __forceinline__ EdgeJob<R> edge_job(const IterParams<R, VT> &P, const R *__restrict__ src, int e,
+                                               int tid, int m, int n, int m0, int n0, int64_t loff, bool inner,
+                                               bool valid, R mu_u, R mu_v, R sg_u, R sg_v)
+{
+    EdgeJob<R> jb{};
+    int hm, hn, rm, rn;
+    const bool own_edge = e < 4;
+    if (own_edge) {
+        jb.dir = e & 1; jb.uv = e >> 1;
+        hm = m; hn = n;
+        rm = jb.dir == 0 ? m + 1 : m; rn = jb.dir == 1 ? n + 1 : n;
+    } else {
+        const int h = tid / Q;  // halo edge index
+        const bool top = h < 2 * TN;
+        const int hh = top ? h : h - 2 * TN, span = top ? TN : TM;
+        jb.uv = hh / span;
+        jb.hr = hh % span;
+        jb.dir = top ? 0 : 1;
+        hm = top ? m0 - 1 : m0 + jb.hr; hn = top ? n0 + jb.hr : n0 - 1;
+        rm = top ? m0 : hm;             rn = top ? hn : n0;
+    }
+    const int M = P.M, N = P.N;
+    const int64_t MNL = P.MNL;
+    const bool r_inner = rm < M && rn < N && node_interior(P, rm, rn);
+    jb.need = own_edge ? (inner || (valid && r_inner)) : (hm >= 0 && hn >= 0 && r_inner);
+    if (jb.need) {
+        const int uv = jb.uv;
+        const int64_t h = hm + (int64_t)M * hn + loff;
+        const int64_t r = rm + (int64_t)M * rn + loff;
+        jb.u1 = own_edge ? (uv ? mu_v : mu_u) : src[h + MNL * uv];
+        jb.o1 = own_edge ? (uv ? sg_v : sg_u) : src[h + MNL * (2 + uv)];
+        jb.p = src[h + MNL * (5 + jb.dir + 2 * uv)];  // rou plane 5+e
+        jb.o2 = src[r + MNL * (2 + uv)];
+        jb.u2 = src[r + MNL * uv];
+    }
+    return jb;
+}
+
 // One tile of one iteration (absolute iteration `it`, reading state buffer
 // `parity`): node and edge gradients, neighbour scatter, clamped ascent into
 // the other buffer, and the tile's exact partial sums into partial row part_r.
@@ -548,11 +606,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     const int M = P.M, N = P.N;
     const int64_t MNL = P.MNL, MN = (int64_t)M * N;
     const bool valid = m < M && n < N;
-    auto interior = [&](int mm, int nn) {
-        return mm >= 1 && mm <= M - 2 && nn >= P.own_lo && nn < P.own_hi && nn + P.n_off >= 1 &&
-               nn + P.n_off <= P.Ng - 2;
-    };
-    const bool inner = valid && interior(m, n);
+    const bool inner = valid && node_interior(P, m, n);
     const bool lead = kj == 0;  // the lane that owns the node's outputs
     const int K2 = P.K2;
     constexpr bool TAB_LDS = Q > 1 && GQ_TAB_LDS;
@@ -622,42 +676,36 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // the row above / the column to the left.  One edge body, streamed into
         // accumulators and LDS, keeps VGPRs low.
         const int njobs = halo_lane ? 5 : 4;  // wave-uniform
+        // Q >= 4 (small grids, about one wave per SIMD: latency-bound) loads
+        // job e+1's operands before computing job e
+        constexpr bool PREFETCH = Q >= 4;
+        auto job_at = [&](int e) {
+            return edge_job<R, VT, Q, TM, TN>(P, src, e, tid, m, n, m0, n0, MN * l, inner, valid, mu_u, mu_v,
+                                                sg_u, sg_v);
+        };
+        EdgeJob<R> next{};
+        if (PREFETCH) next = job_at(0);
 #pragma unroll 1
         for (int e = 0; e < njobs; ++e) {
-            int dir, uv, hm, hn, rm, rn, hr = 0;
-            const bool own_edge = e < 4;
-            if (own_edge) {
-                dir = e & 1; uv = e >> 1;
-                hm = m; hn = n;
-                rm = dir == 0 ? m + 1 : m; rn = dir == 1 ? n + 1 : n;
+            EdgeJob<R> jb;
+            if (PREFETCH) {
+                jb = next;
+                if (e + 1 < njobs) next = job_at(e + 1);
             } else {
-                const int h = tid / Q;  // halo edge index
-                const bool top = h < 2 * TN;
-                const int hh = top ? h : h - 2 * TN, span = top ? TN : TM;
-                uv = hh / span;
-                hr = hh % span;
-                dir = top ? 0 : 1;
-                hm = top ? m0 - 1 : m0 + hr; hn = top ? n0 + hr : n0 - 1;
-                rm = top ? m0 : hm;          rn = top ? hn : n0;
+                jb = job_at(e);
             }
-            const bool r_inner = rm < M && rn < N && interior(rm, rn);
-            const bool need = own_edge ? (inner || (valid && r_inner)) : (hm >= 0 && hn >= 0 && r_inner);
+            const int dir = jb.dir, uv = jb.uv, hr = jb.hr;
+            const bool own_edge = e < 4;
             Grad<R> g{};
-            if (need) {
-                const int64_t h = hm + (int64_t)M * hn + MN * l;
-                const int64_t r = rm + (int64_t)M * rn + MN * l;
-                const R u1 = own_edge ? (uv ? mu_v : mu_u) : src[h + MNL * uv];
-                const R o1 = own_edge ? (uv ? sg_v : sg_u) : src[h + MNL * (2 + uv)];
-                const R p = src[h + MNL * (5 + dir + 2 * uv)];  // rou plane 5+e
-                const R o2 = src[r + MNL * (2 + uv)];
-                const EdgeCoef<R> c = edge_coef(u1, src[r + MNL * uv], o1, o2, p);
+            if (jb.need) {
+                const EdgeCoef<R> c = edge_coef(jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
                 Sums<R> S = edge_sums_dev(tab, kj, K2, Q, P.epsn, c);
                 if (Q > 1) S = lane_combine<Q>(S);
-                g = edge_epi(S, c, P.lams, P.guard != 0, T, a, o1, o2, p, ENG == 2);
+                g = edge_epi(S, c, P.lams, P.guard != 0, T, a, jb.o1, jb.o2, jb.p, ENG == 2);
                 // the edge owns its correlation: clamped ascent right here
                 // (gqmap_gpu_mixture.m:46), nothing else reads drou
                 if (own_edge && inner && lead)
-                    dst[i + MNL * (5 + e)] = fmin(fmax(p + g.dp * step, -P.corr), P.corr);
+                    dst[i + MNL * (5 + e)] = fmin(fmax(jb.p + g.dp * step, -P.corr), P.corr);
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
