@@ -131,6 +131,7 @@ constexpr int NPLANES = 9;
 constexpr int TRACE_CAP = 8192;
 constexpr int GRAPH_CHUNK = 50;
 constexpr int NFIX = 5;        // fixed slots per block: Energy, sum|dmu_u|, sum|dsig_u|, #nonfinite, AEPE sum
+constexpr int ACC_SLICES = 8;
 constexpr int TRACE_W = 4;     // trace ring columns: Energy, ptdmu, ptdsigma, AEPE (NaN without a truth)
 
 struct Ctl {
@@ -141,6 +142,13 @@ struct Ctl {
     double T;
     double alpha[GQMAP_LMAX];
     double w[GQMAP_LMAX];
+    // fused finalize: the iteration's exact sums as four 32-bit limbs each
+    // (acc[x][q][k] = sum over the blocks b with b % ACC_SLICES == x of limb
+    // k of the block's fix128), added with 64-bit integer atomics --
+    // order-independent -- and cleared by the last workgroup after it reads
+    // them.  One slice per XCD (blocks go round-robin to the 8 XCDs): fewer
+    // atomics on one address when a small grid's workgroups end together.
+    unsigned long long acc[ACC_SLICES][NFIX + GQMAP_LMAX][4];
 };
 
 struct FinParams {
@@ -324,6 +332,49 @@ __device__ __forceinline__ fix128 load_part_agent(const fix128 *parts, int PS, i
     const uint64_t lo = __hip_atomic_load(w + part_word(PS, r, q, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t hi = __hip_atomic_load(w + part_word(PS, r, q, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (fix128)(((unsigned __int128)hi << 64) | lo);
+}
+
+// Fused finalize transport: a block adds its fix128 partial q into Ctl::acc
+// as limbs 0-2 (unsigned 32-bit) and 3 (signed): sum_k limb_k 2^(32k) = v.
+// The limb sums stay far inside int64 (925 blocks x 2^32), and integer adds
+// commute, so the totals do not depend on the arrival order.  Zero limbs are
+// skipped.  (Reading rows of partials instead cost the last workgroup a
+// 256-thread reduction: 2.9 us at 80 rows, 4.0 us at 925.)
+__device__ __forceinline__ void acc_add_agent(unsigned long long *acc4, fix128 v)
+{
+    const unsigned __int128 u = (unsigned __int128)v;
+    const long long limb[4] = {(long long)(uint32_t)u, (long long)(uint32_t)(u >> 32),
+                               (long long)(uint32_t)(u >> 64), (long long)(int32_t)(uint32_t)(u >> 96)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (limb[k] != 0)
+            __hip_atomic_fetch_add(acc4 + k, (unsigned long long)limb[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The last workgroup: Ctl::acc -> tot[] (LDS), then clear acc for the next
+// iteration.  All 256 threads call it.
+__device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long long *sh)
+{
+    const int NPR = F.L > 1 ? NFIX + F.L : NFIX;
+    const int tid = threadIdx.x;
+    constexpr int SL = (NFIX + GQMAP_LMAX) * 4;  // words per slice
+    if (tid < 4 * NPR) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int x = 0; x < ACC_SLICES; ++x) {
+            unsigned long long *a = &F.ctl->acc[0][0][0] + x * SL + tid;
+            t += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sh[tid] = t;
+    }
+    __syncthreads();
+    if (tid < NPR) {
+        fix128 v = 0;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) v = (v << 32) + (fix128)(long long)sh[4 * tid + k];
+        tot[tid] = from_fix(v);
+    }
+    __syncthreads();
 }
 
 // Exact reduction of the per-block (or per-tile) fixed-point partials into
@@ -685,8 +736,14 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         };
         EdgeJob<R> next{};
         if (PREFETCH) next = job_at(0);
-#pragma unroll 1
-        for (int e = 0; e < njobs; ++e) {
+        // Q >= 4 single-pixel engines: a constant trip count, fully unrolled
+        // (independent jobs overlap; ctf 30x40 30.0 -> 28.8 us/it; not the
+        // super engine, which it would push past 256 VGPRs: C4 355 -> 407)
+        constexpr bool JOBS_UNROLLED = Q >= 4 && ENG != 1;
+        constexpr int JOB_UNROLL = JOBS_UNROLLED ? 5 : 1;
+#pragma unroll JOB_UNROLL
+        for (int e = 0; e < (JOBS_UNROLLED ? 5 : njobs); ++e) {
+            if (JOBS_UNROLLED && e >= njobs) continue;
             EdgeJob<R> jb;
             if (PREFETCH) {
                 jb = next;
@@ -786,7 +843,11 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         const int lq = tid - NFIX;  // dalpha of the components this block ran
         if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1))
             v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        store_part_agent(P.partials, P.fin.nblocks, part_r, tid, v);
+        if (P.fused) {
+            if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
+        } else {
+            store_part_agent(P.partials, P.fin.nblocks, part_r, tid, v);
+        }
     }
 }
 
@@ -846,8 +907,8 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
     if (tl_on) tl_row[8] = __builtin_amdgcn_s_memrealtime();
 #endif
     __shared__ double tot[NFIX + GQMAP_LMAX];
-    __shared__ fix128 sh_red[256];
-    fin_reduce(P.fin, tot, sh_red);
+    __shared__ unsigned long long sh_acc[4 * (NFIX + GQMAP_LMAX)];
+    fin_reduce_acc(P.fin, tot, sh_acc);
 #if GQ_TIMELINE
     if (tl_on) tl_row[9] = __builtin_amdgcn_s_memrealtime();
 #endif
