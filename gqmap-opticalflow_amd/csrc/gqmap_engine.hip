@@ -1618,7 +1618,9 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
         if (c->d_I1) (void)hipFree(c->d_I1);
         c->d_VV = c->d_I1 = nullptr;
         const size_t vsz = c->fp32 ? sizeof(float) : vv32 ? sizeof(vvs_t) : sizeof(double);
-        GQ_HIP(hipMalloc(&c->d_VV, (size_t)(Mo + 2) * (No + 2) * vsz));
+        // zero tail past the padded frame (gqmap_math.h vv_elems, axis_cell_abs)
+        GQ_HIP(hipMalloc(&c->d_VV, vv_elems(Mo, No) * vsz));
+        GQ_HIP(hipMemset(c->d_VV, 0, vv_elems(Mo, No) * vsz));
         GQ_HIP(hipMalloc(&c->d_I1, (size_t)Mo * No * c->rsz));
         gqmap_status s = alloc_grid(c);
         if (s != GQMAP_OK) return s;

@@ -244,21 +244,31 @@ GQ_HD R bicubic_cell4(VP VV, uint32_t o, uint32_t M2, R so, R to)
 
 GQ_HD uint32_t cell_elem(int iy, int ix, int M2) { return (uint32_t)(iy - 1) + GQ_UMUL24(M2, ix - 1); }
 
+// Elements of a padded-frame (VV) buffer: the (Mo+2) x (No+2) frame, then
+// zeros -- one column and a few elements (VV_TAIL, axis_cell_abs: the taps of
+// cell (Mo, No) reach element (Mo+2) * (No+3)).
+constexpr int VV_TAIL = 8;
+constexpr size_t vv_elems(int Mo, int No) { return (size_t)(Mo + 2) * (size_t)(No + 3) + VV_TAIL; }
+
 // One axis of sample()'s position arithmetic at the absolute 1-based
 // position X on an axis of n pixels -> 1-based cell ix and fraction fr
 // (fp64: the reference's own arithmetic: clamp to [1, n], floor).
+//
+// At X == n the reference's interp2 uses cell n-1 at fraction 1; here it is
+// cell n at fraction 0 (no cap).  Both give the same value: the Keys weights
+// are keys4(1) = (+0, +0, 2, +0) and keys4(0) = (+0, 2, +0, +0), so either
+// fma chain is exactly 2 x the tap in column (row) n plus signed zeros from
+// finite taps -- equal up to the sign of a zero result, which the residual
+// I - v/4 and its square never see.  Cell n reads one tap past the padded
+// frame (column No+2, row Mo+2): VV buffers carry a zero column and a few
+// zero elements past the (Mo+2) x (No+2) frame (vv_elems).
 template <bool CLAMP = true>
 GQ_HD void axis_cell_abs(double X, int n, int &ix, double &fr)
 {
     // min(max(.,1),N) with MATLAB's NaN-ignoring max/min (IEEE maxNum/minNum)
     if (CLAMP) X = fmin(fmax(X, 1.0), (double)n);
-    ix = (int)X;  // X >= 1: truncation == floor
-    if (CLAMP) {
-        ix = ix > n - 1 ? n - 1 : ix;
-        fr = X - (double)ix;
-    } else {
-        fr = GQ_FRACT(X);  // X - floor(X): the same value (X >= 1, no cap)
-    }
+    ix = (int)X;       // X >= 1: truncation == floor
+    fr = GQ_FRACT(X);  // X - floor(X)
 }
 // 1-based pixel j displaced by x (fp64: X = j + x, the reference's form).
 template <bool CLAMP = true>
@@ -274,8 +284,7 @@ GQ_HD void axis_cell(int j, float x, int n, int &ix, float &fr)
     if (CLAMP) x = fminf(fmaxf(x, (float)(1 - j)), (float)(n - j));
     const float f = floorf(x);
     fr = x - f;
-    ix = j + (int)f;
-    if (CLAMP && ix > n - 1) { ix = n - 1; fr = 1.f; }
+    ix = j + (int)f;  // cell n at fraction 0 for x = n - j: see axis_cell_abs
 }
 
 // Relative form for both precisions: integer cell + fraction of the

@@ -107,6 +107,7 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
     w.tab.assign(tabd.begin(), tabd.end());
     const size_t nvv = (size_t)(w.Mo + 2) * (w.No + 2), ni = (size_t)w.Mo * w.No;
     w.VV.assign(VV, VV + nvv);
+    w.VV.resize(vv_elems(w.Mo, w.No), R(0));  // zero tail (axis_cell_abs)
     w.I1.assign(I1, I1 + ni);
     double *planes_in[9] = {S->muu, S->muv, S->sigu, S->sigv, S->pn, S->rou, S->rou + MNL,
                             S->rou + 2 * MNL, S->rou + 3 * MNL};
@@ -341,3 +342,44 @@ extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)
 
 // the device's deterministic exp as a plain function (orc_set_map_exp)
 extern "C" double emu_gq_exp(double x) { return gq_exp(x); }
+
+// sample4_abs (fp64) / sample4 (fp32 relative form) at one position, for the
+// cap identity test (tests/test_spec_identities.py): cap = 0 is the kernel's
+// axis arithmetic (cell n at fraction 0 for X == n); cap = 1 the reference's
+// interp2 cell choice (cell n-1 at fraction 1), same Keys fma chains.
+template <typename R>
+static R emu_sample_t(const std::vector<R> &V, int Mo, int No, double X, double Y, int cap)
+{
+    const int M2 = Mo + 2;
+    if (!cap) {
+        if (sizeof(R) == 8)
+            return (R)sample4_abs<true>(V.data(), M2, Mo, No, X, Y);
+        const int jj = (int)std::floor(X), ii = (int)std::floor(Y);
+        return sample4<true>(V.data(), M2, Mo, No, ii, jj, (R)(X - jj), (R)(Y - ii));
+    }
+    auto axis = [](double P, int n, int &ix, R &fr) {
+        P = std::fmin(std::fmax(P, 1.0), (double)n);
+        ix = (int)P;
+        if (ix > n - 1) ix = n - 1;
+        fr = (R)(P - ix);
+    };
+    int ix, iy;
+    R so, to;
+    axis(X, No, ix, so);
+    axis(Y, Mo, iy, to);
+    return bicubic_cell4<R>(V.data(), cell_elem(iy, ix, M2), (uint32_t)M2, so, to);
+}
+extern "C" void emu_sample(const double *VV, int Mo, int No, const double *X, const double *Y, double *out,
+                           int64_t n, int fp32, int cap)
+{
+    const size_t nvv = (size_t)(Mo + 2) * (No + 2);
+    if (fp32) {
+        std::vector<float> V(VV, VV + nvv);
+        V.resize(vv_elems(Mo, No), 0.f);
+        for (int64_t i = 0; i < n; ++i) out[i] = emu_sample_t<float>(V, Mo, No, X[i], Y[i], cap);
+    } else {
+        std::vector<double> V(VV, VV + nvv);
+        V.resize(vv_elems(Mo, No), 0.0);
+        for (int64_t i = 0; i < n; ++i) out[i] = emu_sample_t<double>(V, Mo, No, X[i], Y[i], cap);
+    }
+}

@@ -271,6 +271,23 @@ def emu_math(fn: int, x) -> np.ndarray:
     return out
 
 
+def emu_sample(VV, Mo: int, No: int, X, Y, fp32: bool = False, cap: bool = False) -> np.ndarray:
+    """4 x interp2-cubic of the padded frame VV at absolute 1-based positions
+    (X column, Y row) through the kernel's axis arithmetic (gqmap_math.h
+    sample4_abs / sample4), or with cap=True the reference's interp2 cell
+    choice at the last column / row (cell n-1 at fraction 1)."""
+    VV = _f64(VV)
+    X = _f64(np.asarray(X, dtype=np.float64).ravel())
+    Y = _f64(np.asarray(Y, dtype=np.float64).ravel())
+    out = np.zeros_like(X)
+    f = lib().emu_sample
+    f.restype = None
+    f.argtypes = [C.POINTER(C.c_double), C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                  C.POINTER(C.c_double), C.c_int64, C.c_int, C.c_int]
+    f(_p(VV), Mo, No, _p(X), _p(Y), _p(out), X.size, int(fp32), int(cap))
+    return out
+
+
 # ---- coarse-to-fine plumbing (gqmap_pyramid_oracle.c) -----------------------
 def resize_len(n: int, scale: float) -> int:
     f = lib().orc_resize_len

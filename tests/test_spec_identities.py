@@ -47,3 +47,38 @@ def test_fract_identity():
                          np.nextafter(np.arange(2.0, 100.0), 0.0)])
     for x in xs:
         assert x - float(int(x)) == x - math.floor(x)
+
+
+def test_last_cell_identity():
+    # axis_cell_abs / axis_cell without the cap: a sample clamped to the last
+    # column / row (X == No, Y == Mo) interpolates cell n at fraction 0 instead
+    # of the reference's cell n-1 at fraction 1 -- the same value (up to the
+    # sign of a zero), fp64 and fp32, with zero, negative and fractional taps
+    import oracle.oracle as O
+    rng = np.random.default_rng(2)
+    for Mo, No in ((7, 9), (16, 20), (5, 5)):
+        for kind in ("int", "frac", "zeros"):
+            if kind == "int":
+                I2 = rng.integers(0, 256, (Mo, No)).astype(np.float64)
+            elif kind == "frac":
+                I2 = rng.normal(0.0, 50.0, (Mo, No))
+            else:
+                I2 = np.zeros((Mo, No))
+                I2[rng.integers(0, Mo, 4), rng.integers(0, No, 4)] = -3.0
+            VV = O.get_vv(np.asfortranarray(I2))
+            n = 4000
+            X = rng.uniform(-5.0, No + 5.0, n)
+            Y = rng.uniform(-5.0, Mo + 5.0, n)
+            sel = rng.integers(0, 4, n)
+            X[sel == 1] = No
+            Y[sel == 2] = Mo
+            X[sel == 3], Y[sel == 3] = No, Mo
+            X[:8] = [No, No + 1e-9, No - 1e-12, 1.0, No, 0.5, No, No]
+            Y[:8] = [Mo, 2.5, Mo, Mo, 1.0, Mo, Mo - 0.5, Mo + 3.0]
+            for fp32 in (False, True):
+                if fp32 and kind == "frac":
+                    continue  # fp32 frames hold exact (integer) values
+                a = O.emu_sample(VV, Mo, No, X, Y, fp32=fp32, cap=False)
+                b = O.emu_sample(VV, Mo, No, X, Y, fp32=fp32, cap=True)
+                assert np.all(np.isfinite(a))
+                np.testing.assert_array_equal(a, b)
