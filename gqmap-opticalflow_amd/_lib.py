@@ -23,7 +23,7 @@ LMAX, KMAX = 8, 16
 # Every entry point declared in include/gqmap.h (checked by tests/test_abi.py).
 EXPORTS = (
     "gqmap_options_default", "gqmap_options_alpha_mode", "gqmap_create", "gqmap_set_images", "gqmap_init_state",
-    "gqmap_set_state", "gqmap_get_state", "gqmap_run", "gqmap_run_aepe", "gqmap_set_truth", "gqmap_run_timed", "gqmap_get_info",
+    "gqmap_set_state", "gqmap_get_state", "gqmap_run", "gqmap_run_aepe", "gqmap_set_truth", "gqmap_run_timed", "gqmap_prepare", "gqmap_get_info",
     "gqmap_get_map", "gqmap_log_p", "gqmap_synchronize", "gqmap_destroy", "gqmap_projsplx",
     "gqmap_mixture_map", "gqmap_flow_to_color", "gqmap_gauss_hermite", "gqmap_rand_uniform",
     "gqmap_last_error", "gqmap_abi_version", "gqmap_device_count", "gqmap_imresize",
@@ -103,6 +103,7 @@ def load():
         "gqmap_run_aepe": (C.c_int, [vp, C.c_int, P(C.c_int), _D, _D]),
         "gqmap_set_truth": (C.c_int, [vp, _D, C.c_int, C.c_int]),
         "gqmap_run_timed": (C.c_int, [vp, C.c_int, P(C.c_int), _D, _D]),
+        "gqmap_prepare": (C.c_int, [vp]),
         "gqmap_get_info": (C.c_int, [vp, P(GqmapInfo)]),
         "gqmap_get_map": (C.c_int, [vp, _D]),
         "gqmap_log_p": (C.c_int, [vp, _D, _D]),

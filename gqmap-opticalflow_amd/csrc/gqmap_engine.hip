@@ -2112,6 +2112,22 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     return GQMAP_OK;
 }
 
+gqmap_status gqmap_prepare(gqmap_ctx *c)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    GQ_CHECK(c->have_images && c->have_state, GQMAP_ERR_STATE, "gqmap_prepare before images/state");
+    GQ_CHECK(c->n_tiles == 1 || c->comm, GQMAP_ERR_STATE,
+             "tile %d/%d: attach RCCL (gqmap_tile_attach_rccl) or use gqmap_tile_group_run", c->tile,
+             c->n_tiles);
+    DeviceGuard dg(c->device);
+    gqmap_status s = ensure_graph(c);
+    if (s != GQMAP_OK) return s;
+    GQ_HIP(hipGraphUpload(c->graph, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    return GQMAP_OK;
+}
+
 gqmap_status gqmap_get_info(gqmap_ctx *c, gqmap_info *info)
 {
     clear_error();

@@ -233,6 +233,10 @@ class Engine:
                                        C.byref(ker)), "gqmap_run_timed")
         return done.value, tot.value, ker.value
 
+    def prepare(self) -> None:
+        """Build and upload the replayed iteration graph now (gqmap_prepare)."""
+        check(self.lib.gqmap_prepare(self.ctx), "gqmap_prepare")
+
     def synchronize(self) -> None:
         check(self.lib.gqmap_synchronize(self.ctx), "gqmap_synchronize")
 

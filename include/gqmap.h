@@ -148,6 +148,9 @@ gqmap_status gqmap_set_truth(gqmap_ctx *ctx, const double *grdt, int Mg, int Ng)
 gqmap_status gqmap_run_aepe(gqmap_ctx *ctx, int n_iter, int *n_done, double *trace, double *aepe);
 gqmap_status gqmap_run_timed(gqmap_ctx *ctx, int n_iter, int *n_done, double *total_ms,
                              double *iter_kernel_ms);
+/* Capture and upload the replayed iteration graph now (gqmap_run otherwise
+ * builds it on its first call of >= 50 iterations): no iteration runs. */
+gqmap_status gqmap_prepare(gqmap_ctx *ctx);
 gqmap_status gqmap_get_info(gqmap_ctx *ctx, gqmap_info *info);
 /* Current mean |mu| flow (L==1) or mixture MAP (L>1, device get_map) as an
  * M x N x 2 field -- the `map` of gqmap_gpu_mixture.m:53-58. */

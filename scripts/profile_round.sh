@@ -20,6 +20,7 @@ run trace --kernel-trace --stats || exit $?
 run fetch --pmc FETCH_SIZE || exit $?
 run write --pmc WRITE_SIZE || exit $?
 if [ ! -f gpurun_out/$TAG/calib_fetch/run_counter_collection.csv ]; then
+  [ -x scripts/micro/fetch_calib ] || hipcc --offload-arch=gfx950 -O2 scripts/micro/fetch_calib.hip -o scripts/micro/fetch_calib || exit $?
   for ctr in FETCH_SIZE WRITE_SIZE; do
     low=$(echo $ctr | cut -d_ -f1 | tr A-Z a-z)
     timeout -k 10 120 rocprofv3 --pmc $ctr -d gpurun_out/$TAG/calib_$low -o run --output-format csv -- \

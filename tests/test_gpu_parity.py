@@ -286,6 +286,25 @@ def test_graph_replay_equals_per_iteration_launches(monkeypatch):
         np.testing.assert_array_equal(getattr(a[2], k), getattr(b[2], k), err_msg=k)
 
 
+def test_prepared_graph_and_timed_replay_are_bit_identical():
+    # bench.py's two legs: gqmap_prepare + gqmap_run (the timed region) and
+    # gqmap_run_timed (per-launch HIP events) from the same initial state
+    from gqmap_opticalflow_amd import Engine
+    I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 388, 584)
+    with Engine(o, I1, I2) as eng:
+        eng.set_state(st)
+        eng.prepare()
+        done, _ = eng.run(70)
+        a = eng.get_state()
+        eng.set_state(st)
+        done2, total_ms, kernel_ms = eng.run_timed(70)
+        b = eng.get_state()
+    assert done == done2 == 70
+    assert 0 < kernel_ms <= total_ms
+    for k in G.STATE_KEYS:
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+
+
 def test_stop_inside_a_graph_chunk():
     # the stop rule (ptdmu < tor, gqmap_gpu_mixture.m:75) firing inside a
     # replayed 50-iteration graph: the remaining launches are no-ops, the
