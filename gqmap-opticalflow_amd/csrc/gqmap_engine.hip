@@ -506,6 +506,14 @@ __device__ void fin_apply(const FinParams &F, const double *tot)
 // the single-scale engine moved arrays to scratch (C2 +24%); bounding the
 // super engine to 2 made its block sum 25% slower than the allocator's own
 // 2-wave (<= 256 VGPR) schedule.  GQ_MIN_WAVES / GQ_SUPER_WAVES: experiments.
+// smallest lanes-per-node split whose edge jobs prefetch the next job's
+// operands / run fully unrolled (experiments: GQ_PREFETCH_MIN_Q, GQ_UNROLL_MIN_Q)
+#ifndef GQ_PREFETCH_MIN_Q
+#define GQ_PREFETCH_MIN_Q 2
+#endif
+#ifndef GQ_UNROLL_MIN_Q
+#define GQ_UNROLL_MIN_Q 2
+#endif
 #ifndef GQ_SUPER_WAVES
 #define GQ_SUPER_WAVES 1
 #endif
@@ -729,7 +737,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         const int njobs = halo_lane ? 5 : 4;  // wave-uniform
         // Q >= 4 (small grids, about one wave per SIMD: latency-bound) loads
         // job e+1's operands before computing job e
-        constexpr bool PREFETCH = Q >= 4;
+        constexpr bool PREFETCH = Q >= GQ_PREFETCH_MIN_Q;
         auto job_at = [&](int e) {
             return edge_job<R, VT, Q, TM, TN>(P, src, e, tid, m, n, m0, n0, MN * l, inner, valid, mu_u, mu_v,
                                                 sg_u, sg_v);
@@ -739,7 +747,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // Q >= 4 single-pixel engines: a constant trip count, fully unrolled
         // (independent jobs overlap; ctf 30x40 30.0 -> 28.8 us/it; not the
         // super engine, which it would push past 256 VGPRs: C4 355 -> 407)
-        constexpr bool JOBS_UNROLLED = Q >= 4 && ENG != 1;
+        constexpr bool JOBS_UNROLLED = Q >= GQ_UNROLL_MIN_Q && ENG != 1;
         constexpr int JOB_UNROLL = JOBS_UNROLLED ? 5 : 1;
 #pragma unroll JOB_UNROLL
         for (int e = 0; e < (JOBS_UNROLLED ? 5 : njobs); ++e) {
