@@ -105,3 +105,11 @@ def test_mex_gateways_build_and_reject_bad_calls_without_a_device():
     for name in ("mixture", "super", "ctf"):
         with pytest.raises(RuntimeError, match="usage"):
             Gateway(name)(1, dict(its=1))
+
+
+def test_context_calls_reject_a_null_context_before_touching_a_device():
+    from gqmap_opticalflow_amd import _lib
+    lib = _lib.load()
+    for call in (lambda: lib.gqmap_prepare(None), lambda: lib.gqmap_synchronize(None)):
+        assert call() == 1  # GQMAP_ERR_INVALID_ARG
+        assert b"null" in lib.gqmap_last_error()
