@@ -734,7 +734,13 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // edges, then job 4 on the halo lanes: the edges entering the tile from
         // the row above / the column to the left.  One edge body, streamed into
         // accumulators and LDS, keeps VGPRs low.
-        const int njobs = halo_lane ? 5 : 4;  // wave-uniform
+        // Wave-uniform for Q = 1, 4, 16 (HALO_LANES = 64, 128, 256); for Q = 2
+        // it is 96, so wave 1 diverges on the halo job.  That is safe because
+        // nothing wave-wide runs inside a job: the only cross-lane op is
+        // lane_combine<Q>, an xor butterfly inside one node's Q adjacent
+        // lanes, and a node's lanes are all halo lanes or none (asserted).
+        static_assert(HALO_LANES % Q == 0, "a node's lanes share their job count");
+        const int njobs = halo_lane ? 5 : 4;
         // Q >= 4 (small grids, about one wave per SIMD: latency-bound) loads
         // job e+1's operands before computing job e
         constexpr bool PREFETCH = Q >= GQ_PREFETCH_MIN_Q;
@@ -1103,6 +1109,7 @@ struct gqmap_ctx {
     fix128 *d_partials = nullptr;
     double *d_trace = nullptr;
     double *d_truth = nullptr;  // gqmap_set_truth: M x N x 2 (ctf engine)
+    size_t truth_elems = 0;     // doubles d_truth was allocated for
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
@@ -1622,13 +1629,23 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
     c->vv32 = vv32;
     if (resize) {
         drop_graph(c);
+        // every buffer below may still be read by work queued on the context
+        // stream (a replayed graph): drain it before freeing
+        GQ_HIP(hipStreamSynchronize(c->stream));
         if (c->d_VV) (void)hipFree(c->d_VV);
         if (c->d_I1) (void)hipFree(c->d_I1);
         c->d_VV = c->d_I1 = nullptr;
+        // a truth belongs to the previous grid (k_iter indexes it with M, N)
+        if (c->d_truth) (void)hipFree(c->d_truth);
+        c->d_truth = nullptr;
+        c->truth_elems = 0;
         const size_t vsz = c->fp32 ? sizeof(float) : vv32 ? sizeof(vvs_t) : sizeof(double);
-        // zero tail past the padded frame (gqmap_math.h vv_elems, axis_cell_abs)
+        // zero tail past the padded frame (gqmap_math.h vv_elems, axis_cell_abs).
+        // Stream-ordered: the context stream is non-blocking, so a null-stream
+        // memset would be unordered with the VV upload / convert_device that
+        // follows on c->stream (round-2 fp64-VV race).
         GQ_HIP(hipMalloc(&c->d_VV, vv_elems(Mo, No) * vsz));
-        GQ_HIP(hipMemset(c->d_VV, 0, vv_elems(Mo, No) * vsz));
+        GQ_HIP(hipMemsetAsync(c->d_VV, 0, vv_elems(Mo, No) * vsz, c->stream));
         GQ_HIP(hipMalloc(&c->d_I1, (size_t)Mo * No * c->rsz));
         gqmap_status s = alloc_grid(c);
         if (s != GQMAP_OK) return s;
@@ -1867,13 +1884,16 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
     gqmap_status s = prepare_images(c, Mo, No, vv32);
     if (s != GQMAP_OK) return s;
     DeviceGuard dg(c->device);
+    // every copy on the context stream, after prepare_images' zero fill
     if (vv32 && !c->fp32) {
         std::vector<vvs_t> vc(VV.size());
         for (size_t k = 0; k < VV.size(); ++k) vc[k] = (vvs_t)VV[k];
-        GQ_HIP(hipMemcpy(c->d_VV, vc.data(), vc.size() * sizeof(vvs_t), hipMemcpyHostToDevice));
+        GQ_HIP(hipMemcpyAsync(c->d_VV, vc.data(), vc.size() * sizeof(vvs_t), hipMemcpyHostToDevice, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
     } else if (vv32) {
         std::vector<float> v32(VV.begin(), VV.end());
-        GQ_HIP(hipMemcpy(c->d_VV, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice));
+        GQ_HIP(hipMemcpyAsync(c->d_VV, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
     } else if ((s = upload(c, c->d_VV, VV.data(), VV.size())) != GQMAP_OK) {
         return s;
     }
@@ -2009,10 +2029,14 @@ gqmap_status gqmap_set_truth(gqmap_ctx *c, const double *grdt, int Mg, int Ng)
              "per-iteration AEPE is the ctf level engine's (legacy/gqmap_ctf.m:38)");
     GQ_CHECK(c->n_tiles == 1, GQMAP_ERR_UNSUPPORTED, "gqmap_set_truth on a column-strip tile");
     DeviceGuard dg(c->device);
-    drop_graph(c);  // the captured launches hold the previous truth pointer
     if (!grdt) {
-        if (c->d_truth) GQ_HIP(hipFree(c->d_truth));
+        if (c->d_truth) {
+            drop_graph(c);  // the captured launches hold the truth pointer
+            GQ_HIP(hipStreamSynchronize(c->stream));
+            GQ_HIP(hipFree(c->d_truth));
+        }
         c->d_truth = nullptr;
+        c->truth_elems = 0;
         return GQMAP_OK;
     }
     GQ_CHECK(Mg >= c->M && Ng >= c->N, GQMAP_ERR_INVALID_ARG, "truth %dx%d smaller than the grid %dx%d", Mg, Ng,
@@ -2025,7 +2049,17 @@ gqmap_status gqmap_set_truth(gqmap_ctx *c, const double *grdt, int Mg, int Ng)
         for (int n = 0; n < c->N; ++n)
             std::memcpy(&blk[MN * k + (size_t)c->M * n], grdt + (size_t)Mg * Ng * k + (size_t)Mg * n,
                         sizeof(double) * c->M);
-    if (!c->d_truth) GQ_HIP(hipMalloc((void **)&c->d_truth, sizeof(double) * 2 * MN));
+    if (c->truth_elems != 2 * MN) {
+        // (re)allocate for this grid; the captured graph holds the old pointer
+        // (a same-size update keeps pointer and graph)
+        drop_graph(c);
+        GQ_HIP(hipStreamSynchronize(c->stream));
+        if (c->d_truth) (void)hipFree(c->d_truth);
+        c->d_truth = nullptr;
+        c->truth_elems = 0;
+        GQ_HIP(hipMalloc((void **)&c->d_truth, sizeof(double) * 2 * MN));
+        c->truth_elems = 2 * MN;
+    }
     GQ_HIP(hipMemcpyAsync(c->d_truth, blk.data(), sizeof(double) * 2 * MN, hipMemcpyHostToDevice, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     return GQMAP_OK;
@@ -2249,6 +2283,36 @@ int gqmap_selftest_math(int fn, const double *in, double *out, int64_t n)
     return e == hipSuccess ? GQMAP_OK : GQMAP_ERR_HIP;
 }
 
+// Not in the public header: the padded frame VV (getVV, gqmap_gpu_mixture.m:
+// 191-208) as the kernels will read it, widened to double; *stored_f32 = 1
+// when it is held in float.  Tests pin that VV == getVV(I2) after
+// gqmap_set_images / ctx_set_images_device (the round-2 upload race).
+gqmap_status gqmap_debug_read_vv(gqmap_ctx *c, double *out, size_t n, int *stored_f32)
+{
+    clear_error();
+    GQ_CHECK(c && out, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "no images");
+    const size_t nvv = (size_t)(c->Mo + 2) * (c->No + 2);
+    GQ_CHECK(n >= nvv, GQMAP_ERR_INVALID_ARG, "buffer holds %zu of %zu values", n, nvv);
+    DeviceGuard dg(c->device);
+    const bool f32 = c->fp32 || c->vv32;
+    if (stored_f32) *stored_f32 = f32;
+    if (!f32) {
+        GQ_HIP(hipMemcpyAsync(out, c->d_VV, nvv * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+        return GQMAP_OK;
+    }
+    const size_t esz = c->fp32 ? sizeof(float) : sizeof(vvs_t);
+    std::vector<unsigned char> raw(nvv * esz);
+    GQ_HIP(hipMemcpyAsync(raw.data(), c->d_VV, raw.size(), hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    for (size_t k = 0; k < nvv; ++k) {
+        if (c->fp32) out[k] = ((const float *)raw.data())[k];
+        else out[k] = (double)((const vvs_t *)raw.data())[k];
+    }
+    return GQMAP_OK;
+}
+
 gqmap_status gqmap_synchronize(gqmap_ctx *c)
 {
     clear_error();
@@ -2275,7 +2339,8 @@ static gqmap_status attach_common(gqmap_ctx *c)
 {
     const size_t NP = NFIX + c->L;
     GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles));
-    GQ_HIP(hipMemset(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles));
+    GQ_HIP(hipMemsetAsync(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
     c->own_gathered = true;
     c->nranks = c->n_tiles;
     drop_graph(c);

@@ -177,7 +177,10 @@ struct Resampler {
     double *w[2] = {nullptr, nullptr};
     int *idx[2] = {nullptr, nullptr};
 
-    gqmap_status build(int M, int N, double scale, int antialias)
+    // the tables are uploaded on stream s, the stream apply() will run on
+    // (the pyramid's stream is non-blocking: null-stream copies would not be
+    // ordered with it)
+    gqmap_status build(int M, int N, double scale, int antialias, hipStream_t s)
     {
         release();
         const int len[2] = {M, N};
@@ -191,8 +194,9 @@ struct Resampler {
             P[d] = resize_contrib(len[d], out_len[d], scale, antialias, hw, hi);
             GQ_HIP(hipMalloc(&w[d], hw.size() * sizeof(double)));
             GQ_HIP(hipMalloc(&idx[d], hi.size() * sizeof(int)));
-            GQ_HIP(hipMemcpy(w[d], hw.data(), hw.size() * sizeof(double), hipMemcpyHostToDevice));
-            GQ_HIP(hipMemcpy(idx[d], hi.data(), hi.size() * sizeof(int), hipMemcpyHostToDevice));
+            GQ_HIP(hipMemcpyAsync(w[d], hw.data(), hw.size() * sizeof(double), hipMemcpyHostToDevice, s));
+            GQ_HIP(hipMemcpyAsync(idx[d], hi.data(), hi.size() * sizeof(int), hipMemcpyHostToDevice, s));
+            GQ_HIP(hipStreamSynchronize(s));  // hw / hi are host temporaries
         }
         return GQMAP_OK;
     }
@@ -346,7 +350,7 @@ gqmap_status gqmap_imresize(const double *in, int M, int N, int C, double scale,
     GQ_CHECK(scale > 0 && std::isfinite(scale), GQMAP_ERR_INVALID_ARG, "gqmap_imresize: scale %g", scale);
     DeviceGuard dg(device);
     Resampler r;
-    gqmap_status st = r.build(M, N, scale, antialias);
+    gqmap_status st = r.build(M, N, scale, antialias, nullptr);
     if (st != GQMAP_OK) {
         r.release();
         return st;
@@ -468,9 +472,9 @@ gqmap_status gqmap_ctf_set_images(gqmap_pyramid *p, const double *img1, const do
         GQ_HIP(hipMalloc(&L.I1w, mn * sizeof(double)));
         GQ_HIP(hipMalloc(&L.warp, 2 * mn * sizeof(double)));
         GQ_HIP(hipMalloc(&L.flow, 2 * mn * sizeof(double)));
-        gqmap_status s = L.img.build(M, N, L.scale, 1);
+        gqmap_status s = L.img.build(M, N, L.scale, 1, p->stream);
         if (s != GQMAP_OK) return s;
-        s = L.pro.build(l ? Ml[l - 1] : M0, l ? Nl[l - 1] : N0, 2.0, 1);
+        s = L.pro.build(l ? Ml[l - 1] : M0, l ? Nl[l - 1] : N0, 2.0, 1, p->stream);
         if (s != GQMAP_OK) return s;
         // I1 = imresize(img_1, scale); I2 = imresize(img_2, scale)  (:26-27)
         GQ_HIP(L.img.apply(p->img[0], 1, 1.0, p->scratch, L.I1, p->stream));
@@ -599,6 +603,18 @@ gqmap_status gqmap_ctf_get_trace(gqmap_pyramid *p, int level, int *n, double *en
     if (energy) std::copy(L.energy.begin(), L.energy.end(), energy);
     if (aepe) std::copy(L.aepe.begin(), L.aepe.end(), aepe);
     return GQMAP_OK;
+}
+
+// Not in the public header: level `level`'s padded frame as its engine reads
+// it (gqmap_debug_read_vv of the level context).
+gqmap_status gqmap_debug_read_vv(gqmap_ctx *c, double *out, size_t n, int *stored_f32);
+gqmap_status gqmap_ctf_debug_read_vv(gqmap_pyramid *p, int level, double *out, size_t n, int *stored_f32)
+{
+    clear_error();
+    GQ_CHECK(p, GQMAP_ERR_INVALID_ARG, "null pyramid");
+    GQ_CHECK(level >= 0 && level < p->nlev, GQMAP_ERR_INVALID_ARG, "level %d of %d", level, p->nlev);
+    GQ_CHECK(p->ran, GQMAP_ERR_STATE, "gqmap_ctf_debug_read_vv before gqmap_ctf_run");
+    return gqmap_debug_read_vv(p->lev[level].ctx, out, n, stored_f32);
 }
 
 void gqmap_ctf_destroy(gqmap_pyramid *p)

@@ -14,15 +14,25 @@
 #include <mex.h>
 
 #include <cmath>
+#include <cstdio>
 #include <vector>
 
 #include "gqmap.h"
 
 namespace {
 
+// The context of the running call: mexErrMsgIdAndTxt longjmps out of the
+// gateway, so fail() releases it (and its device buffers) first.
+gqmap_ctx *g_ctx = nullptr;
+
 void fail(gqmap_status s, const char *what)
 {
-    if (s != GQMAP_OK) mexErrMsgIdAndTxt("gqmap:error", "%s: %s", what, gqmap_last_error());
+    if (s == GQMAP_OK) return;
+    char msg[512];
+    std::snprintf(msg, sizeof msg, "%s: %s", what, gqmap_last_error());
+    if (g_ctx) gqmap_destroy(g_ctx);
+    g_ctx = nullptr;
+    mexErrMsgIdAndTxt("gqmap:error", "%s", msg);
 }
 
 double field_d(const mxArray *opt, const char *name, bool required = true, double dflt = 0)
@@ -74,6 +84,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[])
 
     gqmap_ctx *ctx = nullptr;
     fail(gqmap_create(&ctx, &o, 0), "gqmap_create");
+    g_ctx = ctx;
     fail(gqmap_set_images(ctx, mxGetPr(prhs[1]), mxGetPr(prhs[2]), M, N), "gqmap_set_images");
     fail(gqmap_init_state(ctx, seed), "gqmap_init_state");
     fail(gqmap_set_truth(ctx, G, Mg, Ng), "gqmap_set_truth");
@@ -99,6 +110,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[])
     s.pn = s.sigv + MN; s.rou = s.pn + MN; s.w = s.rou + 4 * MN; s.alpha = s.w + 1;
     fail(gqmap_get_state(ctx, &s), "gqmap_get_state");
     gqmap_destroy(ctx);
+    g_ctx = nullptr;
     mwSize d3[3] = {(mwSize)M, (mwSize)N, 2};
     plhs[0] = mxCreateNumericArray(3, d3, mxDOUBLE_CLASS, mxREAL);
     std::copy(s.muu, s.muu + 2 * MN, mxGetPr(plhs[0]));

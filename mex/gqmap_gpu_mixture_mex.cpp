@@ -27,9 +27,18 @@ constexpr int CROP = 1;  // interior M_, N_ (gqmap_gpu_mixture.m:64)
 #endif
 constexpr int EVAL_EVERY = 300;
 
+// The context of the running call: mexErrMsgIdAndTxt longjmps out of the
+// gateway, so fail() releases it (and its device buffers) first.
+gqmap_ctx *g_ctx = nullptr;
+
 void fail(gqmap_status s, const char *what)
 {
-    if (s != GQMAP_OK) mexErrMsgIdAndTxt("gqmap:error", "%s: %s", what, gqmap_last_error());
+    if (s == GQMAP_OK) return;
+    char msg[512];
+    std::snprintf(msg, sizeof msg, "%s: %s", what, gqmap_last_error());
+    if (g_ctx) gqmap_destroy(g_ctx);
+    g_ctx = nullptr;
+    mexErrMsgIdAndTxt("gqmap:error", "%s", msg);
 }
 
 double field_d(const mxArray *opt, const char *name, bool required = true, double dflt = 0)
@@ -89,6 +98,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[])
 
     gqmap_ctx *ctx = nullptr;
     fail(gqmap_create(&ctx, &o, 0), "gqmap_create");
+    g_ctx = ctx;
     fail(gqmap_set_images(ctx, mxGetPr(prhs[1]), mxGetPr(prhs[2]), Mo, No), "gqmap_set_images");
     fail(gqmap_init_state(ctx, seed), "gqmap_init_state");
     gqmap_info info;
@@ -180,6 +190,7 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[])
     s.pn = s.sigv + MNL; s.rou = s.pn + MNL; s.w = s.rou + 4 * MNL; s.alpha = s.w + L;
     fail(gqmap_get_state(ctx, &s), "gqmap_get_state");
     gqmap_destroy(ctx);
+    g_ctx = nullptr;
     mwSize d4[4] = {(mwSize)M, (mwSize)N, (mwSize)L, 2};
     plhs[0] = mxCreateNumericArray(4, d4, mxDOUBLE_CLASS, mxREAL);
     std::copy(s.muu, s.muu + 2 * MNL, mxGetPr(plhs[0]));
