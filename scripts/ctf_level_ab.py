@@ -3,6 +3,7 @@ libgqmap variants (GQMAP_LIB): k_iter us/it (HIP events, 100 its after 10)
 and a checksum of the final state.  usage: ctf_level_ab.py [fp64|fp32] [scales]"""
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
@@ -21,5 +22,12 @@ for s in scales:
         e.run_timed(10)
         done, tot, ker = e.run_timed(100)
         chk = float(np.sum(e.get_state().muu))
+        e.init_state(0)
+        e.run(10)
+        e.prepare()
+        t0 = time.perf_counter()
+        n, _ = e.run(100)  # production path: replayed graphs, wall clock per iteration
+        e.synchronize()
+        wall = (time.perf_counter() - t0) / n * 1e6
         print(f"scale {s:6.4f} {a.shape[0]:4d}x{a.shape[1]:<4d} Q={e.info().split:2d} "
-              f"k_iter {ker / done * 1e3:7.1f} us/it chk={chk!r}", flush=True)
+              f"k_iter {ker / done * 1e3:7.1f} us/it wall {wall:7.1f} us/it chk={chk!r}", flush=True)
