@@ -12,7 +12,11 @@ frames and state are resident in HBM before the timed region.
 
 Multi-GPU (default) is frame-parallel (weak scaling): every rank solves its
 own 584x388 pair on its own GPU, no data-path collective; `value` is the
-pixels of all ranks x steps / the slowest rank's time.
+pixels of all ranks x steps / the slowest rank's time.  The same line carries
+`strong_scaling`: the RubberWhale pair itself split into one column strip per
+rank (RCCL ghost-column + exact-totals exchange every iteration, lanes per
+node chosen from one strip: gqmap_opticalflow_amd.strip_split), timed the
+same way -- the north star's "584x388 pair at 1, 2, 4 and 8 MI355X".
 
 The other BASELINE configs are selectable (same JSON line, their workload
 named in `config`):
@@ -109,8 +113,11 @@ def host_cpus():
 
 
 def _timed_leg(run_n, budget_s):
-    """Time run_n(n) on a bounded sample: one probe iteration sizes n to
-    about budget_s seconds.  Returns (iterations, seconds)."""
+    """Time run_n(n) on a bounded sample: one untimed warm-up iteration (the
+    first call pays OpenMP start-up and first-touch page faults: 2.7 s once
+    on the GPU box), one probe iteration that sizes n to about budget_s
+    seconds, then n timed iterations.  Returns (iterations, seconds)."""
+    run_n(1)
     t0 = time.perf_counter()
     run_n(1)
     t1 = time.perf_counter() - t0
@@ -120,7 +127,7 @@ def _timed_leg(run_n, budget_s):
     return done, time.perf_counter() - t0
 
 
-def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 8.0):
+def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 8.0, allcores: bool = False):
     """The oracle (literal C fp64 restatement of the engine loop, OpenMP over
     rows) on this host's cores -- every core this process may use, then one
     thread -- on a bounded sample of the same workload."""
@@ -131,7 +138,10 @@ def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 8.0
     M, N = (Mo // 4, No // 4) if engine == "super" else (Mo, No)
     o = dict(opts, engine=engine)
     legs = {}
-    for threads in (hc["threads"], 1):
+    counts = [hc["threads"], 1]
+    if allcores and hc["physical_cores"] and hc["physical_cores"] != hc["threads"]:
+        counts.append(min(hc["physical_cores"], hc["affinity"]))
+    for threads in counts:
         st0 = initial_state(o, M, N, seed=0, engine=engine)
         st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
         it = [1]
@@ -142,8 +152,12 @@ def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 8.0
             return done
         legs[threads] = _timed_leg(run_n, budget_s)
     (n_all, t_all), (n_one, t_one) = legs[hc["threads"]], legs[1]
+    extra = {}
+    if len(counts) > 2:
+        n_pc, t_pc = legs[counts[2]]
+        extra = {"value_allcores": Mo * No * n_pc / t_pc / 1e9, "cores_allcores": counts[2]}
     return {"value": Mo * No * n_all / t_all / 1e9, "unit": "Gpixel-iter/s", "cores": hc["threads"],
-            "kind": "port", "value_1thread": Mo * No * n_one / t_one / 1e9,
+            "kind": "port", "value_1thread": Mo * No * n_one / t_one / 1e9, **extra,
             "nproc": hc["nproc"], "affinity_cpus": hc["affinity"], "physical_cores": hc["physical_cores"],
             "sample": f"oracle/gqmap_oracle.c fp64 ({engine}), {label} {No}x{Mo}, L={opts['L']} K={opts['K']}, "
                       f"seeded init: {n_all} iterations on {hc['threads']} OpenMP threads in {t_all:.1f}s "
@@ -308,7 +322,11 @@ def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
     """One frame as column-strip tiles over the ranks (gqmap_create_tile):
     RCCL ghost-column and exact-totals exchange every iteration.  Returns the
     rank's timing and its share of the AEPE sums (interior pixels)."""
-    from gqmap_opticalflow_amd import Engine, comm_unique_id
+    from gqmap_opticalflow_amd import Engine, comm_unique_id, strip_split
+    Mo, No = I1.shape
+    # lanes per node from ONE strip (the whole-grid solve with the same split
+    # is bit-identical: tests/test_gpu_tiles.py)
+    opts = dict(opts, split=int(opts.get("split") or strip_split(Mo, No, world)))
     eng = Engine(opts, I1, I2, "mixture", args.precision, device=local, n_tiles=world, tile=rank)
     try:
         if world > 1:
@@ -316,18 +334,26 @@ def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
             dist.broadcast_object_list(uid, src=0)
             eng.attach_rccl(uid[0])
         eng.init_state(seed=1)
-        if args.warmup:
-            eng.run(args.warmup)
+        # warm-up with single launches (fewer than a 50-iteration graph chunk):
+        # the RCCL peer connections are set up before any graph capture
+        eng.run(max(1, min(args.warmup, 49)))
+        eng.prepare()  # the replayed graph (kernels + RCCL exchange) captured and uploaded untimed
         eng.init_state(seed=0)  # timed steps are iterations 1..steps of the solve
         barrier()
         t0 = time.perf_counter()
-        done, total_ms, kernel_ms = eng.run_timed(args.steps)
+        done, _ = eng.run(args.steps)  # production path: graph replay
         barrier()
         elapsed = time.perf_counter() - t0
         if done != args.steps:
             raise RuntimeError(f"rank {rank}: solver stopped after {done}/{args.steps} iterations")
         mp = eng.map()
         col0, col1 = eng.col0, eng.col1
+        # k_iter durations: a replay of the same iterations with HIP events
+        # around the boundary + interior launches of every iteration
+        eng.init_state(seed=0)
+        done2, total_ms, kernel_ms = eng.run_timed(args.steps)
+        if done2 != args.steps or not np.array_equal(eng.map(), mp):
+            raise RuntimeError(f"rank {rank}: the instrumented replay differs from the timed run")
     finally:
         eng.close()
     Mo, No = I1.shape
@@ -337,7 +363,7 @@ def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
     f[unk] = 0
     e = np.sqrt(((flo[sl] - f[sl]) ** 2).sum(axis=2))
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, pixels=Mo * No, nodes=Mo * (col1 - col0),
-                err_sum=float(e.sum()), err_n=int(e.size))
+                err_sum=float(e.sum()), err_n=int(e.size), split=opts["split"])
 
 
 def run_tiled(args, rank, world, local, barrier, dist, names, scale, label):
@@ -356,6 +382,7 @@ def run_tiled(args, rank, world, local, barrier, dist, names, scale, label):
         Mo, No = I1.shape
         for k in ("elapsed", "kernel_ms", "pixels", "nodes"):
             tot[k] += r[k]
+        tot["split"] = r["split"]
         tot["pix_its"] += Mo * No * args.steps
         per_pair.append(dict(name=name, size=f"{No}x{Mo}", err_sum=r["err_sum"], err_n=r["err_n"],
                              elapsed=r["elapsed"]))
@@ -369,7 +396,8 @@ def run_tiled(args, rank, world, local, barrier, dist, names, scale, label):
                             f"(imresize(imread(..),scale), optical_flow_temp.m:7-8), GT x{scale:g} in size and "
                             f"value; " if scale != 1 else "")
                          + f"mixture L=1 K=9, each pair as {world} column-strip tile(s) with RCCL ghost-column + "
-                           f"totals exchange per iteration, its={args.steps} per pair, pairs run in turn")
+                           f"totals exchange per iteration, Q={tot['split']} lanes per node (from one strip), "
+                           f"its={args.steps} per pair, pairs run in turn")
 
 
 def main():
@@ -380,6 +408,11 @@ def main():
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"))
     ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c4", "c5"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strong-scaling", action="store_true",
+                    help="c2: skip the strong-scaling leg (the pair split over the ranks)")
+    ap.add_argument("--cpu-allcores", action="store_true",
+                    help="add a CPU-baseline leg on every physical core (off by default: a GPU box grants "
+                         "each GPU a share of its cores through OMP_NUM_THREADS)")
     ap.add_argument("--tiled", action="store_true",
                     help="c2: strong scaling -- the RubberWhale pair split into column strips over the ranks")
     args = ap.parse_args()
@@ -453,6 +486,7 @@ def main():
             p["aepe"] = sums[i] / sums[n + i]
         r["aepe"] = float(np.mean([p["aepe"] for p in r["per_pair"]]))
 
+    out = None
     if rank == 0:
         if cfg == "c3":
             units = r["pix_its"] * world
@@ -510,16 +544,61 @@ def main():
                 out["ms_per_step_instrumented"] = r["instrumented_ms"] / args.steps
         if tiled:
             out["per_pair"] = [{k: p[k] for k in ("name", "size", "aepe", "elapsed")} for p in r["per_pair"]]
-        if not args.no_cpu_baseline and cfg == "c1":
+            out["config"]["split"] = r["split"]
+
+    printed = []
+
+    def emit():
+        if rank == 0 and not printed:
+            printed.append(1)
+            print(json.dumps(out), flush=True)
+
+    if cfg == "c2" and not tiled and not args.no_strong_scaling:
+        # the headline pair split over the ranks (strong scaling).  A watchdog
+        # keeps a stuck exchange from costing the whole line: after its limit
+        # rank 0 prints what it has and every rank leaves.
+        limit = float(os.environ.get("GQMAP_STRONG_TIMEOUT", "180"))
+
+        def fire():
+            if out is not None:
+                out["strong_scaling"] = {"error": f"no result within {limit:.0f} s (watchdog)"}
+            emit()
+            os._exit(0)
+        import threading
+        wd = threading.Timer(limit, fire)
+        wd.daemon = True
+        wd.start()
+        try:
+            st = run_tiled(args, rank, world, local, barrier, dist, ("rubberwhale",), 1.0, "C2 strong scaling")
+            te, tk = st["elapsed"], st["kernel_ms"]
+            if dist is not None:
+                t = torch.tensor([te, tk], device=dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                te, tk = t.tolist()
+            if out is not None:
+                pp = st["per_pair"][0]
+                out["strong_scaling"] = {
+                    "value": st["pix_its"] / te / 1e9, "unit": "Gpixel-iter/s", "n_gpus": world,
+                    "ms_per_step": te / args.steps * 1e3, "k_iter_us": tk / args.steps * 1e3,
+                    "scaling": "strong", "split": st["split"], "parallelism": f"column-strip tiles x{world} (RCCL halo)",
+                    "workload": f"rubberwhale {pp['size']} mixture L=1 K=9 its={args.steps}, one column strip per "
+                                f"rank, Q={st['split']} lanes per node (from one strip)",
+                    "aepe": None}
+        except Exception as e:  # reported in the line; the frame-parallel value stands
+            if out is not None:
+                out["strong_scaling"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the CPU baseline is a rank-0, N=1 figure (bench contract)
+        if cfg == "c1":
             out["cpu_baseline"] = cpu_baseline_c1(r["flow"], r["opts"])
-        elif not args.no_cpu_baseline:
+        else:
             lab = {"c2": "RubberWhale", "c3": "Grove3 full-resolution level", "c4": "Urban3",
                    "c5": "Urban3 x4"}[cfg]
             I1c, I2c, oc = r["I1"], r["I2"], r["opts"]
             if cfg == "c5":  # bounded sample: a 388x584 window of the upsampled frame
                 I1c, I2c = (np.asfortranarray(a[600:988, 900:1484]) for a in (I1c, I2c))
-            out["cpu_baseline"] = cpu_baseline(I1c, I2c, oc, engine, lab)
-        print(json.dumps(out), flush=True)
+            out["cpu_baseline"] = cpu_baseline(I1c, I2c, oc, engine, lab, allcores=args.cpu_allcores)
+    emit()
     if dist is not None:
         dist.destroy_process_group()
 
