@@ -358,13 +358,17 @@ __device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long lo
     const int tid = threadIdx.x;
     constexpr int SL = (NFIX + GQMAP_LMAX) * 4;  // words per slice
     if (tid < 4 * NPR) {
+        // all slices' loads in flight together, then the clears (one memory
+        // round trip instead of eight: finalize 2.9 -> ~1 us)
+        unsigned long long *a = &F.ctl->acc[0][0][0] + tid;
+        unsigned long long v[ACC_SLICES];
+#pragma unroll
+        for (int x = 0; x < ACC_SLICES; ++x) v[x] = __hip_atomic_load(a + x * SL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long t = 0;
 #pragma unroll
-        for (int x = 0; x < ACC_SLICES; ++x) {
-            unsigned long long *a = &F.ctl->acc[0][0][0] + x * SL + tid;
-            t += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (int x = 0; x < ACC_SLICES; ++x) t += v[x];
+#pragma unroll
+        for (int x = 0; x < ACC_SLICES; ++x) __hip_atomic_store(a + x * SL, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sh[tid] = t;
     }
     __syncthreads();
@@ -546,7 +550,11 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
 
 // Node rows of a tile with Q lanes per node (256 / Q nodes): 16 x 16, 16 x 8
 // (two 16-row columns per wave), 8 x 8, 4 x 4; lanes are m-fastest.
-constexpr int tile_rows(int q) { return q <= 2 ? 16 : q == 4 ? 8 : 4; }
+// Q = 64 (k_iter_wn): one wave per node, WN_TM waves per workgroup, tiles of
+// WN_TM x 1 nodes.
+constexpr int WN_TM = 5;
+constexpr int tile_rows(int q) { return q <= 2 ? 16 : q == 4 ? 8 : q == 64 ? WN_TM : 4; }
+constexpr int tile_cols(int q) { return q == 64 ? 1 : BLOCK / q / tile_rows(q); }
 
 // LDS of one tile: in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n);
 // in_left: from (m,n-1); red: per-wave partial sums.  Declared by the kernels
@@ -638,6 +646,74 @@ __device__ __forceinline__ EdgeJob<R> edge_job(const IterParams<R, VT> &P, const
         jb.u2 = src[r + MNL * uv];
     }
     return jb;
+}
+
+// The clamped ascent of one interior node from its assembled gradients
+// (gqmap_gpu_mixture.m:41-45; gqmap_ctf.m:34-35), the updated state into dst
+// and the node's exact contributions to the block sums; returns its dalpha.
+template <int ENG, typename R, typename VT>
+__device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__restrict__ dst, int64_t i, int m,
+                                             int n, R step, R mu_u, R mu_v, R sg_u, R sg_v, R pn, const Grad<R> &nd,
+                                             R gmu_u, R gmu_v, R gsg_u, R gsg_v, R eE, R eda, fix128 &fE,
+                                             fix128 &fmu, fix128 &fsg, fix128 &fae, int &nonfinite)
+{
+    const int M = P.M;
+    const int64_t MNL = P.MNL, MN = (int64_t)M * P.N;
+    auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
+    const R nu = cl(mu_u + gmu_u * step, P.minu, P.maxu), nv = cl(mu_v + gmu_v * step, P.minv, P.maxv);
+    dst[i + MNL * 0] = nu;
+    dst[i + MNL * 1] = nv;
+    if constexpr (ENG == 2) {  // AEPE of gqmap_ctf.m:38 against the updated mean
+        if (P.truth) {
+            const double du = P.truth[m + (int64_t)M * n] - (double)nu;
+            const double dv = P.truth[m + (int64_t)M * n + MN] - (double)nv;
+            fae += to_fix(gq_sqrt_dev(du * du + dv * dv));
+        }
+    }
+    // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
+    const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
+    const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
+    dst[i + MNL * 2] = cl(sg_u + su, P.sig_lo, P.sig_hi);
+    dst[i + MNL * 3] = cl(sg_v + sv, P.sig_lo, P.sig_hi);
+    dst[i + MNL * 4] = cl(pn + nd.dp * step, -P.corr, P.corr);
+    // per-node contributions to the global sums (exact fixed point)
+    const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
+    const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
+    nonfinite += !finite_d(cE) + !finite_d(cda) + !finite_d(cmu) + !finite_d(csg);
+    fE += to_fix(cE);
+    fmu += to_fix(cmu);
+    fsg += to_fix(csg);
+    return to_fix(cda);
+}
+
+// Last workgroup of a fused launch (arrival ticket) runs the finalize step;
+// all threads of every workgroup call it after storing their partials.
+__device__ __forceinline__ void fused_finalize_tail(const FinParams &F)
+{
+    Ctl *ctl = F.ctl;
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        last = atomicAdd(&ctl->arrive, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    TL_STAMP(8, __builtin_amdgcn_s_memrealtime());
+    __shared__ double tot[NFIX + GQMAP_LMAX];
+    __shared__ unsigned long long sh_acc[4 * (NFIX + GQMAP_LMAX)];
+    fin_reduce_acc(F, tot, sh_acc);
+    TL_STAMP(9, __builtin_amdgcn_s_memrealtime());
+#if GQ_TIMELINE
+    const int tl_it = ctl->it;
+#endif
+    if (threadIdx.x == 0) {
+        fin_apply(F, tot);
+        ctl->arrive = 0;
+#if GQ_TIMELINE
+        const int d_ = tl_it - GQ_TIMELINE;
+        if ((d_ == 0 || d_ == 1) && blockIdx.x < 8192) g_timeline[32 * blockIdx.x + 16 * d_ + 7] = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
 }
 
 // One tile of one iteration (absolute iteration `it`, reading state buffer
@@ -803,31 +879,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][pix]) + in_left[1][0][pix];
             const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][pix]) + in_left[0][1][pix];
             const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
-            auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
-            const R nu = cl(mu_u + gmu_u * step, P.minu, P.maxu), nv = cl(mu_v + gmu_v * step, P.minv, P.maxv);
-            dst[i + MNL * 0] = nu;
-            dst[i + MNL * 1] = nv;
-            if constexpr (ENG == 2) {  // AEPE of gqmap_ctf.m:38 against the updated mean
-                if (P.truth) {
-                    const double du = P.truth[m + (int64_t)M * n] - (double)nu;
-                    const double dv = P.truth[m + (int64_t)M * n + MN] - (double)nv;
-                    fae += to_fix(gq_sqrt_dev(du * du + dv * dv));
-                }
-            }
-            // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
-            const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
-            const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
-            dst[i + MNL * 2] = cl(sg_u + su, P.sig_lo, P.sig_hi);
-            dst[i + MNL * 3] = cl(sg_v + sv, P.sig_lo, P.sig_hi);
-            dst[i + MNL * 4] = cl(pn + nd.dp * step, -P.corr, P.corr);
-            // per-node contributions to the global sums (exact fixed point)
-            const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
-            const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
-            nonfinite += !finite_d(cE) + !finite_d(cda) + !finite_d(cmu) + !finite_d(csg);
-            fE += to_fix(cE);
-            fda = to_fix(cda);
-            fmu += to_fix(cmu);
-            fsg += to_fix(csg);
+            fda = node_apply<ENG>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u, gsg_v,
+                                  eE, eda, fE, fmu, fsg, fae, nonfinite);
         }
         if (P.L > 1) {  // dalpha(l): only consumed by the alpha update
             fda = wave_sum_fix(fda);
@@ -933,6 +986,163 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT
         if (tl_on) tl_row[7] = __builtin_amdgcn_s_memrealtime();
 #endif
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Smallest grids (below 2^13 nodes: the coarse pyramid levels): one wave per
+// node (Q = 64).  A workgroup's four waves take four nodes of one column
+// (tile = 4 x 1 nodes).  Per node and component:
+//   node   the K^2 points over the wave's 64 lanes + a 6-level butterfly;
+//   round 1  its four own edges (down/right x u/v), one per 16-lane group
+//          (the Q = 16 edge order, edge_parts), the edge owner's clamped rou
+//          update;
+//   round 2  the four edges entering it (from the node above / to the left),
+//          again one per group -- the neighbour recomputes nothing for it and
+//          no LDS or grid exchange is needed;
+// then the update of the node.  The work of the round-2 edges is done twice
+// (by the owner for its rou and du1/do1, by the tail node for du2/do2), which
+// costs nothing here: each wave's dependent chain is one node's 2 points +
+// two edge jobs instead of 8 points + five jobs at Q = 16 (the lanes are
+// idle otherwise at this size).  Same bits as the CPU model with split 64.
+// Five waves per workgroup: the 30 x 40 level's 1200 nodes make 240
+// workgroups, one per CU (with four, 300 workgroups put two on 44 CUs and
+// those set the end of the launch).
+// ---------------------------------------------------------------------------
+constexpr int WN_THREADS = 64 * WN_TM;
+
+template <typename R>
+struct WnLds {
+    fix128 red[GQMAP_LMAX + NFIX][WN_TM];
+    R tab[NTAB * TS];
+};
+
+template <typename R, typename VT, int ENG>
+__global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
+{
+    Ctl *ctl = P.ctl;
+    if (ctl->stop) return;
+#if GQ_TIMELINE
+    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int nb = P.seg_n[0] + P.seg_n[1];
+    const int b = blockIdx.x;
+    const int tl = tile_of_block(b, nb, 1, P.cu_slots);
+    const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
+    __shared__ WnLds<R> lds;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int grp = lane >> 4, gl = lane & 15;  // 16-lane group of the edge jobs
+    const int K2 = P.K2;
+    const int it = ctl->it, parity = ctl->done & 1;
+    const R *__restrict__ src = parity ? P.st1 : P.st0;
+    R *__restrict__ dst = parity ? P.st0 : P.st1;
+    const R T = R(ctl->T);
+    const R step = R(P.step0 / (1.0 + it / P.step_decay));
+    const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
+    const int m = tm * WN_TM + wave, n = tn;
+    const int M = P.M, N = P.N;
+    const int64_t MNL = P.MNL, MN = (int64_t)M * N;
+    const bool inner = m < M && n < N && node_interior(P, m, n);  // wave-uniform
+    fix128 fE = 0, fmu = 0, fsg = 0, fae = 0;
+    int nonfinite = 0;
+    auto &red = lds.red;
+    const R *tab = lds.tab;
+
+    for (int l = 0; l < P.L; ++l) {
+        fix128 fda = 0;
+        const int64_t i = m + (int64_t)M * n + MN * l;
+        const int dir = grp & 1, uv = grp >> 1;
+        const int64_t r = dir == 0 ? i + 1 : i + M;  // own edge: tail node (m+1,n) / (m,n+1)
+        const int64_t h = dir == 0 ? i - 1 : i - M;  // entering edge: head node (m-1,n) / (m,n-1)
+        // this node's state and the operands of the lane group's two edge
+        // jobs, loaded before the table copy's barrier
+        R mu_u = 0, mu_v = 0, sg_u = 0, sg_v = 0, pn = 0, p1 = 0, u2 = 0, o2 = 0, p2 = 0, hu = 0, ho = 0;
+        if (inner) {
+            mu_u = src[i]; mu_v = src[i + MNL]; sg_u = src[i + MNL * 2]; sg_v = src[i + MNL * 3];
+            pn = src[i + MNL * 4];
+            p1 = src[i + MNL * (5 + grp)]; u2 = src[r + MNL * uv]; o2 = src[r + MNL * (2 + uv)];
+            p2 = src[h + MNL * (5 + grp)]; hu = src[h + MNL * uv]; ho = src[h + MNL * (2 + uv)];
+        }
+        if (l == 0) {
+            for (int e = tid; e < NTAB * K2; e += WN_THREADS) lds.tab[e] = P.tab[e];
+            __syncthreads();
+            TL_STAMP(1, __builtin_amdgcn_s_memrealtime());
+        }
+        if (inner) {
+            const R a = R(ctl->alpha[l]);
+            const R own_u = uv ? mu_v : mu_u, own_o = uv ? sg_v : sg_u;
+            // node: 64 lanes
+            const NodeCoef<R> c = node_coef(sg_u, sg_v, pn);
+            Sums<R> S = node_sums<ENG, true>(tab, lane, K2, 64, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c, mu_u,
+                                             mu_v, m, n + P.n_off);
+            S = lane_combine<64>(S);
+            const Grad<R> nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, sg_u, sg_v, pn, ENG == 2);
+            // round 1: own edge e = grp (dir + 2 uv), Q = 16 in the group
+            const EdgeCoef<R> c1 = edge_coef(own_u, u2, own_o, o2, p1);
+            Sums<R> S1 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c1);
+            S1 = lane_combine<16>(S1);
+            const Grad<R> g1 = edge_epi(S1, c1, P.lams, P.guard != 0, T, a, own_o, o2, p1, ENG == 2);
+            if (gl == 0) dst[i + MNL * (5 + grp)] = fmin(fmax(p1 + g1.dp * step, -P.corr), P.corr);
+            // round 2: the edge entering from the head node h (its edge grp)
+            const EdgeCoef<R> c2 = edge_coef(hu, own_u, ho, own_o, p2);
+            Sums<R> S2 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c2);
+            S2 = lane_combine<16>(S2);
+            const Grad<R> g2 = edge_epi(S2, c2, P.lams, P.guard != 0, T, a, ho, own_o, p2, ENG == 2);
+            // the four groups' results to every lane (group e's values from lane 16 e)
+            auto from = [&](R v, int e) { return __shfl(v, 16 * e, 64); };
+            R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0, eE = 0, eda = 0;
+            // iter_tile's order: edge jobs e = 0..3 accumulated in turn
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const R du1 = from(g1.du1, e), do1 = from(g1.do1, e);
+                if ((e >> 1) == 0) { sum_mu0 = sum_mu0 + du1; sum_sg0 = sum_sg0 + do1; }
+                else               { sum_mu1 = sum_mu1 + du1; sum_sg1 = sum_sg1 + do1; }
+                eE = eE + from(g1.E, e);
+                eda = eda + from(g1.da, e);
+            }
+            // the neighbours' shares: in_up[uv] from group 2 uv (dir 0), in_left[uv] from 2 uv + 1
+            R up[2][2], left[2][2];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                up[v][0] = from(g2.du2, 2 * v); up[v][1] = from(g2.do2, 2 * v);
+                left[v][0] = from(g2.du2, 2 * v + 1); left[v][1] = from(g2.do2, 2 * v + 1);
+            }
+            if (lane == 0) {
+                const R gmu_u = ((nd.du1 + sum_mu0) + up[0][0]) + left[0][0];
+                const R gmu_v = ((nd.du2 + sum_mu1) + up[1][0]) + left[1][0];
+                const R gsg_u = ((nd.do1 + sum_sg0) + up[0][1]) + left[0][1];
+                const R gsg_v = ((nd.do2 + sum_sg1) + up[1][1]) + left[1][1];
+                fda = node_apply<ENG>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u,
+                                      gsg_v, eE, eda, fE, fmu, fsg, fae, nonfinite);
+            }
+        }
+        if (P.L > 1 && lane == 0) red[NFIX + l][wave] = fda;
+        TL_STAMP(2, __builtin_amdgcn_s_memrealtime());
+    }
+    TL_STAMP(3, __builtin_amdgcn_s_memrealtime());
+    // block partials: only lane 0 of each wave holds a node's contributions
+    if (lane == 0) {
+        red[0][wave] = fE;
+        red[1][wave] = fmu;
+        red[2][wave] = fsg;
+        red[3][wave] = (fix128)nonfinite;
+        red[4][wave] = fae;
+    }
+    __syncthreads();
+    const int NP = NFIX + P.L;
+    if (tid < NP) {
+        fix128 v = 0;
+#pragma unroll
+        for (int w = 0; w < WN_TM; ++w) v += red[tid][w];
+        if (P.fused) {
+            if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
+        } else {
+            store_part_agent(P.partials, P.fin.nblocks, P.part_off + b, tid, v);
+        }
+    }
+    TL_STAMP(0, tl0);
+    TL_STAMP(4, __builtin_amdgcn_s_memrealtime());
+    if (P.fused) fused_finalize_tail(P.fin);
 }
 
 __global__ __launch_bounds__(256) void k_finalize(FinParams F)
@@ -1148,15 +1358,18 @@ namespace {
 // 30x40 109/81/53/34, 60x80 112/83/54/43, 120x160 113/87/67/100, 240x320
 // 173/142/145/332, 480x640 302/374/423/1207; C2 (mixture K=9, 388x584)
 // Q=1 173, Q=2 227 -> single-pixel engines: Q = 16 below 2^13 nodes, 4
-// below 2^16, 2 below 2^17, else 1.  The super engine runs its L components as separate blocks
+// below 2^16, 2 below 2^17, else 1; round 3: one wave per node (Q = 64,
+// k_iter_wn) below 2^11 nodes (30x40 26.1 -> 19.1 us; 60x80 35.0 -> 58.6 us,
+// kept at 16).  The super engine runs its L components as separate blocks
 // (choose_lpar) and counts node-components: C4 (120x160 x L=3 = 57,600)
 // Q = 16 / 4 / 1 -> 616 / 509 / 613-717 us with global table reads (one block
 // per tile: 680 / 829 / 1687); Q = 4 with the LDS table 376 us.
 int choose_split(int M, int N, int L, int forced, bool super_)
 {
-    if (forced == 1 || forced == 2 || forced == 4 || forced == 16) return forced;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 16 || (forced == 64 && !super_)) return forced;
     const int64_t nodes = (int64_t)M * N;
-    if (!super_) return nodes >= (1 << 17) ? 1 : nodes >= (1 << 16) ? 2 : nodes >= (1 << 13) ? 4 : 16;
+    if (!super_)
+        return nodes >= (1 << 17) ? 1 : nodes >= (1 << 16) ? 2 : nodes >= (1 << 13) ? 4 : nodes >= (1 << 11) ? 16 : 64;
     const int64_t nl = nodes * L;
     if (nl >= (1 << 17)) return 1;
     if (nl >= (1 << 14)) return 4;
@@ -1187,7 +1400,7 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     // from the whole grid (Ng columns), so every column-strip tile sums its
     // quadrature in the same order as the untiled solve
     c->split = choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
-    const int tr = tile_rows(c->split), tc = BLOCK / c->split / tr;
+    const int tr = tile_rows(c->split), tc = tile_cols(c->split);
     c->tiles_m = (c->M + tr - 1) / tr;
     c->tiles_n = (c->N + tc - 1) / tc;
     c->lpar = choose_lpar(c);
@@ -1294,7 +1507,7 @@ struct TileSegs {
 // [0, bnd) and [bnd, nblocks).
 void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
 {
-    const int TN = BLOCK / c->split / tile_rows(c->split);  // tile columns
+    const int TN = tile_cols(c->split);  // tile columns
     const int tm = c->tiles_m, cb0 = c->own_lo / TN, cb1 = (c->own_hi - 1) / TN;
     bnd.lo[0] = cb0 * tm; bnd.n[0] = tm;
     bnd.lo[1] = cb1 * tm; bnd.n[1] = cb1 != cb0 ? tm : 0;
@@ -1329,9 +1542,33 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
     k_iter<R, VT, ENG, Q><<<nblocks, BLOCK, 0, c->stream>>>(P);
 }
 
+// Q = 64 (one wave per node, k_iter_wn): tiles of 4 x 1 nodes
+template <typename R, typename VT, int ENG>
+void launch_k_iter_wn(gqmap_ctx *c, const TileSegs *sg)
+{
+    IterParams<R, VT> P = iter_params<R, VT>(c);
+    int nblocks = c->nblocks;
+    if (sg) {
+        for (int k = 0; k < 2; ++k) {
+            P.seg_lo[k] = sg->lo[k];
+            P.seg_n[k] = sg->n[k];
+        }
+        P.part_off = sg->part_off;
+        nblocks = sg->n[0] + sg->n[1];
+        if (nblocks == 0) return;
+    }
+    static const int2 shape = kernel_shape(k_iter_wn<R, VT, ENG>);
+    P.cu_group = 1;
+    P.cu_slots = std::max(1, shape.y / 8);
+    k_iter_wn<R, VT, ENG><<<nblocks, WN_THREADS, 0, c->stream>>>(P);
+}
+
 template <typename R, typename VT, int ENG>
 void launch_iter_q(gqmap_ctx *c, const TileSegs *sg)
 {
+    if constexpr (ENG != 1) {
+        if (c->split == 64) return launch_k_iter_wn<R, VT, ENG>(c, sg);
+    }
     if (c->split == 16)
         launch_k_iter<R, VT, ENG, 16>(c, sg);
     else if (c->split == 4)

@@ -589,13 +589,17 @@ GQ_HD Sums<R> sums_plus(const Sums<R> &a, const Sums<R> &b)
     r.sa = a.sa + b.sa; r.sm = a.sm + b.sm; r.sx = a.sx + b.sx;
     return r;
 }
+// Q = 64 is the one-wave-per-node form of the smallest grids: the node's
+// quadrature over the 64 lanes of its wave, each edge over a 16-lane group
+// (edge_parts).
+constexpr int edge_parts(int Q) { return Q > 16 ? 16 : Q; }
 template <typename R>
 GQ_HD Sums<R> butterfly(const Sums<R> *parts, int Q)
 {
-    Sums<R> v[16];
+    Sums<R> v[64];
     for (int j = 0; j < Q; ++j) v[j] = parts[j];
     for (int o = Q / 2; o > 0; o >>= 1) {
-        Sums<R> w[16];
+        Sums<R> w[64];
         for (int j = 0; j < Q; ++j) w[j] = sums_plus(v[j], v[j ^ o]);
         for (int j = 0; j < Q; ++j) v[j] = w[j];
     }

@@ -71,7 +71,7 @@ template <typename F>
 auto split_sums(int Q, F part) -> decltype(part(0, 1))
 {
     if (Q == 1) return part(0, 1);
-    decltype(part(0, 1)) parts[16];
+    decltype(part(0, 1)) parts[64];
     for (int j = 0; j < Q; ++j) parts[j] = part(j, Q);
     return butterfly(parts, Q);
 }
@@ -159,7 +159,8 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                             const R o1 = st[i + MNL * (2 + uv)], o2 = st[r + MNL * (2 + uv)];
                             const R p = st[i + MNL * (5 + e)];
                             const EdgeCoef<R> c = edge_coef(st[i + MNL * uv], st[r + MNL * uv], o1, o2, p);
-                            const Sums<R> Se = split_sums(Q, [&](int k0, int dk) {
+                            // Q = 64 (one wave per node): the edges run on 16-lane groups
+                            const Sums<R> Se = split_sums(edge_parts(Q), [&](int k0, int dk) {
                                 return edge_sums(tab, k0, w.K2, dk, eps, c);
                             });
                             g = edge_epi(Se, c, lams, guard, Tr, a, o1, o2, p, ENG == 2);
@@ -310,7 +311,7 @@ extern "C" int emu_run_tile(const orc_params *P, const double *X, const double *
                             double *trace, int nthreads, int fp32, int split, const int *geo,
                             int64_t *totals)
 {
-    if (split != 1 && split != 2 && split != 4 && split != 16) return -2;
+    if (split != 1 && split != 2 && split != 4 && split != 16 && split != 64) return -2;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
@@ -324,7 +325,7 @@ extern "C" int emu_run(const orc_params *P, const double *X, const double *W, co
                        double *trace, int nthreads, int fp32, int split)
 {
     const int Q = split;
-    if (Q != 1 && Q != 2 && Q != 4 && Q != 16) return -2;
+    if (Q != 1 && Q != 2 && Q != 4 && Q != 16 && Q != 64) return -2;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif

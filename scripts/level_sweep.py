@@ -1,5 +1,5 @@
 """k_iter time per iteration on each C3 pyramid level (Grove3 resized, ctf
-engine K=11) for lanes-per-node Q = 1, 2, 4, 16.  usage: level_sweep.py [fp64|fp32]"""
+engine K=11) for lanes-per-node Q = 1, 2, 4, 16, 64 (QS=... to choose).  usage: level_sweep.py [fp64|fp32]"""
 import os
 import sys
 
@@ -14,7 +14,7 @@ I1, I2, flo, unk, o = gt_options("Grove3", 1, 11)
 for s in C3_SCALES:
     a, b = (np.asfortranarray(imresize(x, s)) for x in (I1, I2))
     res = []
-    for q in (1, 2, 4, 16):
+    for q in [int(x) for x in os.environ.get("QS", "1,2,4,16,64").split(",")]:
         opts = ctf_options(its=500, minu=o["minu"], maxu=o["maxu"], minv=o["minv"], maxv=o["maxv"], split=q)
         with Engine(opts, a, b, "ctf", prec) as e:
             e.init_state(0)

@@ -24,6 +24,8 @@ else:
     I1, I2, flo, unk, g = gt_options("Grove3", 1, 11)
     I1, I2 = (np.asfortranarray(imresize(x, s)) for x in (I1, I2))
     o = ctf_options(its=500, minu=g["minu"], maxu=g["maxu"], minv=g["minv"], maxv=g["maxv"])
+    if os.environ.get("GQMAP_SPLIT"):
+        o["split"] = int(os.environ["GQMAP_SPLIT"])
     engine = "ctf"
 NB = 8192
 with Engine(o, I1, I2, engine, prec) as eng:

@@ -205,7 +205,9 @@ def test_bit_exact_vs_emulator_golden_init(name, precision):
                                                   ("super", 1, 11, 100, 132, 1),
                                                   ("ctf", 1, 11, 96, 128, 1),
                                                   ("ctf", 1, 11, 60, 70, 4),
-                                                  ("ctf", 1, 11, 30, 44, 16)])
+                                                  ("ctf", 1, 11, 30, 44, 16),
+                                                  ("ctf", 1, 11, 30, 44, 64),
+                                                  ("mixture", 3, 9, 30, 44, 64)])
 def test_bit_exact_vs_emulator_reference_init(engine, L, K, M, N, split, precision):
     # reference-style init (pn = rou = 0), many tiles (halo edges across tiles),
     # ragged last tiles, alpha update from iteration 10, every lanes-per-node Q
@@ -261,7 +263,9 @@ def _run_engine(o, I1, I2, engine, precision, st, its):
                                                 ("ctf", 11, 96, 128, 1),
                                                 ("ctf", 11, 96, 128, 2),
                                                 ("ctf", 11, 60, 70, 4),
-                                                ("ctf", 11, 30, 44, 16)])
+                                                ("ctf", 11, 30, 44, 16),
+                                                ("ctf", 11, 30, 44, 64),
+                                                ("mixture", 9, 60, 70, 64)])
 def test_single_gaussian_every_split_bit_exact_vs_emulator(engine, K, M, N, split, precision):
     # L = 1, constant temperature, every lanes-per-node Q (16 x 16, 16 x 8,
     # 8 x 8, 4 x 4 node tiles) against the CPU model
