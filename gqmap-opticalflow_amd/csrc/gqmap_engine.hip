@@ -521,7 +521,15 @@ __device__ void fin_apply(const FinParams &F, const double *tot)
 #ifndef GQ_SUPER_WAVES
 #define GQ_SUPER_WAVES 1
 #endif
-constexpr int min_waves(int eng) { return GQ_MIN_WAVES > 1 ? GQ_MIN_WAVES : eng == 1 ? GQ_SUPER_WAVES : 1; }
+#ifndef GQ_MIDQ_WAVES  // single-pixel engines at Q = 2, 4, 8: waves/SIMD the allocation must allow
+#define GQ_MIDQ_WAVES 1
+#endif
+constexpr int min_waves(int eng, int q)
+{
+    return GQ_MIN_WAVES > 1 ? GQ_MIN_WAVES
+         : eng == 1        ? GQ_SUPER_WAVES
+         : (q >= 2 && q <= 8) ? GQ_MIDQ_WAVES : 1;
+}
 
 // Tile index of block b: XCD-aware order.  Blocks b and b+8 share an XCD
 // (round-robin dispatch), so each XCD gets a contiguous band of tiles (L2
@@ -553,7 +561,7 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
 // Q = 64 (k_iter_wn): one wave per node, WN_TM waves per workgroup, tiles of
 // WN_TM x 1 nodes.
 constexpr int WN_TM = 5;
-constexpr int tile_rows(int q) { return q <= 2 ? 16 : q == 4 ? 8 : q == 64 ? WN_TM : 4; }
+constexpr int tile_rows(int q) { return q <= 2 ? 16 : q <= 8 ? 8 : q == 64 ? WN_TM : 4; }
 constexpr int tile_cols(int q) { return q == 64 ? 1 : BLOCK / q / tile_rows(q); }
 
 // LDS of one tile: in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n);
@@ -810,7 +818,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // edges, then job 4 on the halo lanes: the edges entering the tile from
         // the row above / the column to the left.  One edge body, streamed into
         // accumulators and LDS, keeps VGPRs low.
-        // Wave-uniform for Q = 1, 4, 16 (HALO_LANES = 64, 128, 256); for Q = 2
+        // Wave-uniform for Q = 1, 4, 8, 16 (HALO_LANES = 64, 128, 192, 256); for Q = 2
         // it is 96, so wave 1 diverges on the halo job.  That is safe because
         // nothing wave-wide runs inside a job: the only cross-lane op is
         // lane_combine<Q>, an xor butterfly inside one node's Q adjacent
@@ -920,7 +928,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 
 
 template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(BLOCK, min_waves(ENG)) void k_iter(IterParams<R, VT> P)
+__global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
 {
     Ctl *ctl = P.ctl;
     if (ctl->stop) return;
@@ -1358,18 +1366,19 @@ namespace {
 // 30x40 109/81/53/34, 60x80 112/83/54/43, 120x160 113/87/67/100, 240x320
 // 173/142/145/332, 480x640 302/374/423/1207; C2 (mixture K=9, 388x584)
 // Q=1 173, Q=2 227 -> single-pixel engines: Q = 16 below 2^13 nodes, 4
-// below 2^16, 2 below 2^17, else 1; round 3: one wave per node (Q = 64,
-// k_iter_wn) below 2^11 nodes (30x40 26.1 -> 19.1 us; 60x80 35.0 -> 58.6 us,
-// kept at 16).  The super engine runs its L components as separate blocks
+// below 2^16, 2 below 2^17, else 1; round 3 (profiles/r03_midq_sweep.txt):
+// one wave per node (Q = 64, k_iter_wn) below 2^11 nodes (30x40 26.1 -> 19.1
+// us), Q = 8 (8 x 4 tiles) below 2^13 (60x80 35.0 -> 31.1 us; Q = 64 58.6).  The super engine runs its L components as separate blocks
 // (choose_lpar) and counts node-components: C4 (120x160 x L=3 = 57,600)
 // Q = 16 / 4 / 1 -> 616 / 509 / 613-717 us with global table reads (one block
 // per tile: 680 / 829 / 1687); Q = 4 with the LDS table 376 us.
 int choose_split(int M, int N, int L, int forced, bool super_)
 {
-    if (forced == 1 || forced == 2 || forced == 4 || forced == 16 || (forced == 64 && !super_)) return forced;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 8 || forced == 16 || (forced == 64 && !super_))
+        return forced;
     const int64_t nodes = (int64_t)M * N;
     if (!super_)
-        return nodes >= (1 << 17) ? 1 : nodes >= (1 << 16) ? 2 : nodes >= (1 << 13) ? 4 : nodes >= (1 << 11) ? 16 : 64;
+        return nodes >= (1 << 17) ? 1 : nodes >= (1 << 16) ? 2 : nodes >= (1 << 13) ? 4 : nodes >= (1 << 11) ? 8 : 64;
     const int64_t nl = nodes * L;
     if (nl >= (1 << 17)) return 1;
     if (nl >= (1 << 14)) return 4;
@@ -1571,6 +1580,8 @@ void launch_iter_q(gqmap_ctx *c, const TileSegs *sg)
     }
     if (c->split == 16)
         launch_k_iter<R, VT, ENG, 16>(c, sg);
+    else if (c->split == 8)
+        launch_k_iter<R, VT, ENG, 8>(c, sg);
     else if (c->split == 4)
         launch_k_iter<R, VT, ENG, 4>(c, sg);
     else if (c->split == 2)

@@ -311,7 +311,7 @@ extern "C" int emu_run_tile(const orc_params *P, const double *X, const double *
                             double *trace, int nthreads, int fp32, int split, const int *geo,
                             int64_t *totals)
 {
-    if (split != 1 && split != 2 && split != 4 && split != 16 && split != 64) return -2;
+    if (split != 1 && split != 2 && split != 4 && split != 8 && split != 16 && split != 64) return -2;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif
@@ -325,7 +325,7 @@ extern "C" int emu_run(const orc_params *P, const double *X, const double *W, co
                        double *trace, int nthreads, int fp32, int split)
 {
     const int Q = split;
-    if (Q != 1 && Q != 2 && Q != 4 && Q != 16 && Q != 64) return -2;
+    if (Q != 1 && Q != 2 && Q != 4 && Q != 8 && Q != 16 && Q != 64) return -2;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #endif

@@ -233,7 +233,7 @@ def split_for(M: int, N: int, super_: bool = False, L: int = 1) -> int:
     nodes = M * N
     if not super_:
         return (1 if nodes >= (1 << 17) else 2 if nodes >= (1 << 16) else 4 if nodes >= (1 << 13)
-                else 16 if nodes >= (1 << 11) else 64)
+                else 8 if nodes >= (1 << 11) else 64)
     nodes *= L
     return 1 if nodes >= (1 << 17) else 4 if nodes >= (1 << 14) else 16
 

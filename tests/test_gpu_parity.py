@@ -207,6 +207,7 @@ def test_bit_exact_vs_emulator_golden_init(name, precision):
                                                   ("ctf", 1, 11, 60, 70, 4),
                                                   ("ctf", 1, 11, 30, 44, 16),
                                                   ("ctf", 1, 11, 30, 44, 64),
+                                                  ("ctf", 1, 11, 60, 70, 8),
                                                   ("mixture", 3, 9, 30, 44, 64)])
 def test_bit_exact_vs_emulator_reference_init(engine, L, K, M, N, split, precision):
     # reference-style init (pn = rou = 0), many tiles (halo edges across tiles),
@@ -265,6 +266,8 @@ def _run_engine(o, I1, I2, engine, precision, st, its):
                                                 ("ctf", 11, 60, 70, 4),
                                                 ("ctf", 11, 30, 44, 16),
                                                 ("ctf", 11, 30, 44, 64),
+                                                ("ctf", 11, 60, 70, 8),
+                                                ("mixture", 9, 60, 70, 8),
                                                 ("mixture", 9, 60, 70, 64)])
 def test_single_gaussian_every_split_bit_exact_vs_emulator(engine, K, M, N, split, precision):
     # L = 1, constant temperature, every lanes-per-node Q (16 x 16, 16 x 8,
