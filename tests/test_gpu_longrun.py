@@ -8,12 +8,13 @@ restatement the per-step agreement is ~1e-12 (test_fullsize.py), and the
 solver's chaotic transient amplifies that: a 1e-13 perturbation of the
 initial state already moves iteration 10's Energy by ~2e-6 relative, and
 the end-state AEPE after 300 iterations of the literal restatement itself
-spreads by ~0.002 over such perturbations (2.5061, 2.5041, 2.5046;
-profiles/r03_longrun_spread.txt).  Long-run parity with the reference is
-therefore tolerance-based, with the tolerances written here:
+spreads over 2.504 .. 2.517 (sigma ~0.006) under perturbations of 1e-13 and
+2e-13 (profiles/r03_longrun_spread.txt).  Long-run parity with the reference
+is therefore tolerance-based, with the tolerances written here:
   * iteration 1 (before any amplification): trace within 1e-10 relative;
-  * after 300 iterations: |AEPE(GPU) - AEPE(literal)| <= 0.02 (10x the
-    literal restatement's own spread under 1e-13 perturbations).
+  * after 300 iterations: |AEPE(GPU) - AEPE(literal)| <= 0.02 (about 3 sigma
+    of the literal restatement's own spread).  Both sides are deterministic,
+    so the test is too: it does not flake, it only moves with the spec.
 The stop rule (ptdmu < tor, gqmap_gpu_mixture.m:75) is not pinned by a long
 run: at the reference settings ptdmu stays O(10) for thousands of
 iterations, so no run here stops; the rule itself is tested where it fires
