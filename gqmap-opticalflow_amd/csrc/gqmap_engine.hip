@@ -192,6 +192,12 @@ struct IterParams {
     // reduces the partials and runs the k_finalize step in the same launch
     int fused;
     int lpar;                // 1: a block runs all components of its tile; L: one component per block
+    // lpar > 1, whole-grid fused launch: block b runs component (b >> 3) % L
+    // of the tile of virtual block ((b >> 3) / L) << 3 | (b & 7) -- a tile's
+    // L components on one XCD, back to back (they share its I1 block and
+    // nearby gather windows in that L2); 8 L ceil(tiles / 8) blocks, those
+    // past the last tile idle
+    int lpar_xcd;
     int cu_group, cu_slots;  // co-resident workgroups per CU, CUs per XCD (tile order only)
     FinParams fin;
     R epsn, lamd, lams;
@@ -938,9 +944,16 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     const int nb = P.seg_n[0] + P.seg_n[1];  // tiles in this launch
     const int b = blockIdx.x;
     // lpar > 1: one block per (tile, component), component-major
-    const int bt = P.lpar > 1 ? b % nb : b;
-    const int l0 = P.lpar > 1 ? b / nb : 0, l1 = P.lpar > 1 ? l0 + 1 : P.L;
-    const int tl = tile_of_block(bt, nb, P.cu_group, P.cu_slots);
+    int bt = P.lpar > 1 ? b % nb : b;
+    int l0 = P.lpar > 1 ? b / nb : 0;
+    if (P.lpar_xcd) {
+        const int j = b >> 3, jt = j / P.lpar;
+        l0 = j - jt * P.lpar;
+        bt = (jt << 3) | (b & 7);
+    }
+    const int l1 = P.lpar > 1 ? l0 + 1 : P.L;
+    const bool idle = bt >= nb;  // lpar_xcd padding
+    const int tl = idle ? 0 : tile_of_block(bt, nb, P.cu_group, P.cu_slots);
     const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
     // workgroups that start on one CU are local blocks j, j+S, j+2S of the
     // XCD (see tile_of_block): alternate the phase order among them.  Not
@@ -948,7 +961,9 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
     __shared__ TileLds<R, BLOCK / Q> lds;
     const int part_r = P.part_off + b;
-    if (edge_first)
+    if (idle) {
+        // nothing to compute or add; still takes its arrival ticket below
+    } else if (edge_first)
         iter_tile<R, VT, ENG, Q, true>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1);
     else
         iter_tile<R, VT, ENG, Q, false>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1);
@@ -1467,6 +1482,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.n_off = c->n_off; P.own_lo = c->own_lo; P.own_hi = c->own_hi; P.Ng = c->Ng;
     P.fused = fused_finalize(c);
     P.lpar = c->lpar;
+    P.lpar_xcd = 0;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     return P;
@@ -1547,6 +1563,11 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
         P.cu_slots = std::max(1, shape.y / 8);
         if (const char *g = getenv("GQMAP_CU_GROUP")) P.cu_group = atoi(g);
         if (getenv("GQMAP_CU_GROUP_PRINT")) fprintf(stderr, "k_iter Q=%d cu_group %d cu_slots %d\n", Q, P.cu_group, P.cu_slots);
+    }
+    static const bool lpar_xcd = !getenv("GQMAP_NO_LPAR_XCD");
+    if (c->lpar > 1 && P.fused && !sg && lpar_xcd) {
+        P.lpar_xcd = 1;
+        nblocks = 8 * c->lpar * ((c->tiles_m * c->tiles_n + 7) / 8);
     }
     k_iter<R, VT, ENG, Q><<<nblocks, BLOCK, 0, c->stream>>>(P);
 }

@@ -424,44 +424,69 @@ GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x
             const R d = fma(out[q >> 2][q & 3], R(-0.25), I[q]);  // I - out/4, bit for bit
             f = f + GQ_SQRT(fma(d, d, eps));
         }
-    } else if (sizeof(R) == 4) {
-        for (int q = 0; q < 16; ++q) {
-            const R d = fma(sample4(VV, M2, Mo, No, i0 + (q >> 2) + 1, j0 + (q & 3) + 1, x1, x2), R(-0.25), I[q]);
-            f = f + GQ_SQRT(fma(d, d, eps));
-        }
     } else {
-        // the same per-pixel clamped samples with the per-column cells and
-        // weights (they depend only on dj) and per-row ones computed once:
-        // identical values, C4 fp64 511 -> 402 us/it.  (fp32 keeps the plain
-        // loop: the hoisted form costs it a wave per SIMD, 380 -> 480 us/it.)
-        // axis_cell_rel of each column / row from one floor per axis: the
-        // pixel j's cell is j + floor(x) with fraction x - floor(x) unless it
-        // clamps (j + floor(x) <= 0 -> cell 1, fraction 0; >= n -> cell n-1,
-        // fraction 1) -- the same values, integer compares only
+        // A block that some sample of crosses the border.  Rows: each
+        // pixel row its own clamped cell and weights (axis_cell_rel: cell
+        // i + floor(x2) unless it clamps -- <= 0: cell 1 at fraction 0,
+        // >= Mo: cell Mo-1 at fraction 1 -- from one floor per axis).
+        // Columns: the pixel columns whose cells j0+dj+1+floor(x1) do not
+        // clamp share the window of seven tap columns of the safe branch --
+        // per pixel row, each window column's row chain is computed once and
+        // fed to the pixel columns that use it, in the fma order of
+        // bicubic_w4.  A clamped pixel column has weights keys4(0) =
+        // (+0, 2, +0, +0) at cell 1 or keys4(1) = (+0, +0, 2, +0) at cell
+        // No-1, so its bicubic_w4 chain is exactly 2 x the row chain of tap
+        // column 1 or No (up to the sign of an exact zero, which the residual
+        // I - v/4 and its square never see).  Same values as sixteen
+        // per-pixel bicubic_w4 calls with nine row chains per pixel row
+        // instead of sixteen: C4 k_iter fp64 350 -> 300-327 us, fp32
+        // 344-390 -> 288-322 us (profiles/r03_super_clamped.txt).
         const R fx = floor(x1), fy = floor(x2);
         const R sx = x1 - fx, sy = x2 - fy;
         const int ifx = (int)fx, ify = (int)fy;
-        R sw[4][4];
-        int ixs[4];
-        GQ_UNROLL_FULL
-        for (int dj = 0; dj < 4; ++dj) {
-            const int c = j0 + dj + 1 + ifx;
-            ixs[dj] = c <= 0 ? 1 : c >= No ? No - 1 : c;
-            const R fr = c <= 0 ? R(0) : c >= No ? R(1) : sx;
-            keys4(fr, sw[dj][0], sw[dj][1], sw[dj][2], sw[dj][3]);
-        }
+        R s0, s1, s2, s3;
+        keys4(sx, s0, s1, s2, s3);
+        // pixel rows one at a time (few live registers), in the order of the
+        // residual sum below (q = 4 di + dj)
         GQ_UNROLL_FULL
         for (int di = 0; di < 4; ++di) {
             const int r = i0 + di + 1 + ify;
             const int iy = r <= 0 ? 1 : r >= Mo ? Mo - 1 : r;
-            const R fr = r <= 0 ? R(0) : r >= Mo ? R(1) : sy;
             R t0, t1, t2, t3;
-            keys4(fr, t0, t1, t2, t3);
+            keys4(r <= 0 ? R(0) : r >= Mo ? R(1) : sy, t0, t1, t2, t3);
+            const uint32_t rb = (uint32_t)(iy - 1);
+            // the row chain of padded tap column col (bicubic_w4's v_a)
+            auto chain = [&](int col) {
+                const auto cp = elem_ptr(VV, rb + GQ_UMUL24(M2, col));
+                return fma(R(cp[3]), t3, fma(R(cp[2]), t2, fma(R(cp[1]), t1, R(cp[0]) * t0)));
+            };
+            // branch-free: every window column is evaluated (its index kept
+            // inside the padded frame; a column no unclamped pixel column
+            // reads only feeds outputs that the clamped-column values below
+            // replace), so divergent lanes run one straight-line body
+            R o[4];
+            GQ_UNROLL_FULL
+            for (int a = 0; a < 7; ++a) {
+                int col = j0 + ifx + a;
+                col = col < 0 ? 0 : col > No + 1 ? No + 1 : col;
+                const R v = chain(col);
+                GQ_UNROLL_FULL
+                for (int dj = 0; dj < 4; ++dj) {
+                    const int k = a - dj;  // this column is tap k of pixel column dj
+                    if (k < 0 || k > 3) continue;
+                    const R sk = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+                    o[dj] = k == 0 ? sk * v : fma(sk, v, o[dj]);
+                }
+            }
+            const R vl = R(2) * chain(1), vr = R(2) * chain(No);  // padded tap columns 1 / No
             GQ_UNROLL_FULL
             for (int dj = 0; dj < 4; ++dj) {
-                const R v4 = bicubic_w4<R>(VV, cell_elem(iy, ixs[dj], M2), (uint32_t)M2, sw[dj][0], sw[dj][1],
-                                           sw[dj][2], sw[dj][3], t0, t1, t2, t3);
-                const R d = fma(v4, R(-0.25), I[4 * di + dj]);
+                const int c = j0 + dj + 1 + ifx;
+                o[dj] = c <= 0 ? vl : c >= No ? vr : o[dj];
+            }
+            GQ_UNROLL_FULL
+            for (int dj = 0; dj < 4; ++dj) {
+                const R d = fma(o[dj], R(-0.25), I[4 * di + dj]);
                 f = f + GQ_SQRT(fma(d, d, eps));
             }
         }
