@@ -1369,7 +1369,7 @@ struct gqmap_ctx {
     // RCCL tiles: the ghost-column exchange runs on `side` while the interior
     // tiles run on `stream` (fork / join events)
     hipStream_t side = nullptr;
-    hipEvent_t ev_bnd = nullptr, ev_inr = nullptr, ev_xch = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_bnd = nullptr, ev_inr = nullptr, ev_xch = nullptr;
 };
 
 namespace {
@@ -1745,9 +1745,18 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     TileSegs bnd, inr;
     tile_segments(c, bnd, inr);
     if (e0) GQ_HIP(hipEventRecord(e0, c->stream));
+    // the boundary tile columns on the side stream, at the same time as the
+    // interior tiles on the main stream (a strip's boundary launch alone
+    // holds few workgroups: run back to back the two launches cost two tile
+    // latencies per iteration); their owned columns are packed and
+    // exchanged as soon as they are done
+    GQ_HIP(hipEventRecord(c->ev_fork, c->stream));
+    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    hipStream_t main_stream = c->stream;
+    c->stream = c->side;
     launch_iter(c, &bnd);
-    GQ_HIP(hipEventRecord(c->ev_bnd, c->stream));
-    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_bnd, 0));
+    c->stream = main_stream;
+    GQ_HIP(hipEventRecord(c->ev_bnd, c->side));
     halo_pack(c, c->side);
     GQ_NCCL(R->GroupStart());
     if (left) {
@@ -1760,6 +1769,7 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     }
     GQ_NCCL(R->GroupEnd());
     launch_iter(c, &inr);
+    GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));  // both launches' partial rows
     if (e1) GQ_HIP(hipEventRecord(e1, c->stream));
     k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)r * NP,
                                              c->d_ctl);
@@ -2653,7 +2663,7 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
     gqmap_status s = attach_common(c);
     if (s != GQMAP_OK) return s;
     GQ_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    for (hipEvent_t *e : {&c->ev_bnd, &c->ev_inr, &c->ev_xch})
+    for (hipEvent_t *e : {&c->ev_fork, &c->ev_bnd, &c->ev_inr, &c->ev_xch})
         GQ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     return GQMAP_OK;
 }
@@ -2835,7 +2845,7 @@ void gqmap_destroy(gqmap_ctx *c)
         delete c->comm;
     }
     if (c->side) (void)hipStreamSynchronize(c->side);
-    for (hipEvent_t e : {c->ev_bnd, c->ev_inr, c->ev_xch})
+    for (hipEvent_t e : {c->ev_fork, c->ev_bnd, c->ev_inr, c->ev_xch})
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);
