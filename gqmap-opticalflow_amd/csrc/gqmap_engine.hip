@@ -191,6 +191,12 @@ struct IterParams {
     // fused finalize: the last workgroup to finish (arrival ticket in Ctl)
     // reduces the partials and runs the k_finalize step in the same launch
     int fused;
+    // RCCL tile (not fused): the blocks of the iteration's launches (boundary
+    // + interior, ticket_total in all) add their sums into Ctl::acc like a
+    // fused launch, and the last one writes the tile's exact totals to
+    // tile_totals (this rank's row of the all-gathered table)
+    int tile_acc, ticket_total;
+    fix128 *tile_totals;
     int lpar;                // 1: a block runs all components of its tile; L: one component per block
     // lpar > 1, whole-grid fused launch: block b runs component (b >> 3) % L
     // of the tile of virtual block ((b >> 3) / L) << 3 | (b & 7) -- a tile's
@@ -730,6 +736,45 @@ __device__ __forceinline__ void fused_finalize_tail(const FinParams &F)
     }
 }
 
+// RCCL tile: the last of the iteration's ticket_total workgroups (both the
+// boundary and the interior launch) turns Ctl::acc into the tile's exact
+// totals (fix128, this rank's row of the table the all-gather shares) and
+// clears acc and the ticket.  All threads of every workgroup call it.
+__device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, fix128 *out)
+{
+    Ctl *ctl = F.ctl;
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        last = atomicAdd(&ctl->arrive, 1) == total - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    const int NP = NFIX + F.L, tid = threadIdx.x;
+    constexpr int SL = (NFIX + GQMAP_LMAX) * 4;
+    __shared__ unsigned long long sh[4 * (NFIX + GQMAP_LMAX)];
+    if (tid < 4 * NP) {
+        unsigned long long *a = &ctl->acc[0][0][0] + tid;
+        unsigned long long v[ACC_SLICES];
+#pragma unroll
+        for (int x = 0; x < ACC_SLICES; ++x) v[x] = __hip_atomic_load(a + x * SL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long t = 0;
+#pragma unroll
+        for (int x = 0; x < ACC_SLICES; ++x) t += v[x];
+#pragma unroll
+        for (int x = 0; x < ACC_SLICES; ++x) __hip_atomic_store(a + x * SL, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh[tid] = t;
+    }
+    __syncthreads();
+    if (tid < NP) {
+        fix128 v = 0;
+#pragma unroll
+        for (int k = 3; k >= 0; --k) v = (v << 32) + (fix128)(long long)sh[4 * tid + k];
+        out[tid] = v;
+    }
+    if (tid == 0) ctl->arrive = 0;
+}
+
 // One tile of one iteration (absolute iteration `it`, reading state buffer
 // `parity`): node and edge gradients, neighbour scatter, clamped ascent into
 // the other buffer, and the tile's exact partial sums into partial row part_r.
@@ -924,7 +969,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         const int lq = tid - NFIX;  // dalpha of the components this block ran
         if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1))
             v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        if (P.fused) {
+        if (P.fused || P.tile_acc) {
             if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
         } else {
             store_part_agent(P.partials, P.fin.nblocks, part_r, tid, v);
@@ -975,7 +1020,10 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     TL_STAMP(6, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));
     const int tl_it = ctl->it;
 #endif
-    if (!P.fused) return;
+    if (!P.fused) {
+        if (P.tile_acc) tile_totals_tail(P.fin, P.ticket_total, P.tile_totals);
+        return;
+    }
     const int tid = threadIdx.x;
     // Last workgroup in runs the finalize step: release the partials at
     // device scope (the XCDs' L2s are not coherent), take an arrival ticket,
@@ -1157,7 +1205,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
         fix128 v = 0;
 #pragma unroll
         for (int w = 0; w < WN_TM; ++w) v += red[tid][w];
-        if (P.fused) {
+        if (P.fused || P.tile_acc) {
             if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
         } else {
             store_part_agent(P.partials, P.fin.nblocks, P.part_off + b, tid, v);
@@ -1166,6 +1214,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
     TL_STAMP(0, tl0);
     TL_STAMP(4, __builtin_amdgcn_s_memrealtime());
     if (P.fused) fused_finalize_tail(P.fin);
+    else if (P.tile_acc) tile_totals_tail(P.fin, P.ticket_total, P.tile_totals);
 }
 
 __global__ __launch_bounds__(256) void k_finalize(FinParams F)
@@ -1483,6 +1532,11 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.fused = fused_finalize(c);
     P.lpar = c->lpar;
     P.lpar_xcd = 0;
+    // RCCL tiles: exact totals straight from the k_iter launches (no
+    // k_reduce_local between the launches and the all-gather)
+    P.tile_acc = c->comm != nullptr;
+    P.ticket_total = c->nblocks;
+    P.tile_totals = c->d_gathered ? c->d_gathered + (size_t)c->tile * (NFIX + c->L) : nullptr;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     return P;
@@ -1771,8 +1825,8 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     launch_iter(c, &inr);
     GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));  // both launches' partial rows
     if (e1) GQ_HIP(hipEventRecord(e1, c->stream));
-    k_reduce_local<<<1, 256, 0, c->stream>>>(c->d_partials, c->nblocks, NP, c->d_gathered + (size_t)r * NP,
-                                             c->d_ctl);
+    // (this rank's totals row was written by the last workgroup of the two
+    // launches: tile_totals_tail)
     GQ_HIP(hipEventRecord(c->ev_inr, c->stream));
     GQ_HIP(hipStreamWaitEvent(c->side, c->ev_inr, 0));
     GQ_NCCL(R->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
