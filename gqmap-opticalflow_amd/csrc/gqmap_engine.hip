@@ -1266,12 +1266,25 @@ constexpr int HALO_TO_LEFT_N = 4;
 constexpr uint32_t HALO_TO_RIGHT = 0x863210;   // + rou(dir 2, u), rou(dir 2, v) (planes 6, 8)
 constexpr int HALO_TO_RIGHT_N = 6;
 
+// One side of an exchange: column col <-> buf, planes listed 4 bits each.
 template <typename R>
-__global__ void k_halo_copy(const Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL, int L, int col,
-                            uint32_t planes, int np, R *buf, int to_buf)
+struct HaloSide {
+    int col, np;
+    uint32_t planes;
+    R *buf;
+};
+// Both sides of a pack or unpack in one launch: blockIdx.y picks the side
+// (the strip ends have one; nsides = 1).
+template <typename R>
+__global__ void k_halo_copy(const Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL, int L,
+                            HaloSide<R> s0, HaloSide<R> s1, int to_buf)
 {
     if (ctl->stop) return;
     R *dst = (ctl->done & 1) ? st0 : st1;
+    const HaloSide<R> &hs = blockIdx.y == 0 ? s0 : s1;
+    const int col = hs.col, np = hs.np;
+    const uint32_t planes = hs.planes;
+    R *buf = hs.buf;
     const int64_t n = (int64_t)np * L * M;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
         const int m = (int)(t % M);
@@ -1745,33 +1758,46 @@ struct RcclComm {
 
 namespace {
 
+// sides: the present ones (left and/or right), one launch
 template <typename R>
-void halo_copy(gqmap_ctx *c, hipStream_t s, int col, uint32_t planes, int np, void *buf, bool to_buf)
+void halo_copy(gqmap_ctx *c, hipStream_t s, const HaloSide<R> *sides, int nsides, bool to_buf)
 {
-    const int64_t n = (int64_t)np * c->L * c->M;
+    if (nsides == 0) return;
+    int64_t n = 0;
+    for (int k = 0; k < nsides; ++k) n = std::max<int64_t>(n, (int64_t)sides[k].np * c->L * c->M);
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
-    k_halo_copy<R><<<grid, 256, 0, s>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M, (int64_t)c->M * c->N,
-                                        c->MNL, c->L, col, planes, np, (R *)buf, to_buf);
+    k_halo_copy<R><<<dim3(grid, nsides), 256, 0, s>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M,
+                                                     (int64_t)c->M * c->N, c->MNL, c->L, sides[0],
+                                                     sides[nsides - 1], to_buf);
 }
 
-void halo_move(gqmap_ctx *c, hipStream_t s, int col, uint32_t planes, int np, void *buf, bool to_buf)
+// (column, planes, buffer) of the left / right side; left = the side towards tile - 1
+template <typename R>
+void halo_move(gqmap_ctx *c, hipStream_t s, bool pack)
 {
-    if (c->fp32) halo_copy<float>(c, s, col, planes, np, buf, to_buf);
-    else halo_copy<double>(c, s, col, planes, np, buf, to_buf);
+    HaloSide<R> sd[2];
+    int n = 0;
+    if (c->tile > 0)
+        sd[n++] = pack ? HaloSide<R>{c->own_lo, HALO_TO_LEFT_N, HALO_TO_LEFT, (R *)c->d_halo[0]}
+                       : HaloSide<R>{0, HALO_TO_RIGHT_N, HALO_TO_RIGHT, (R *)c->d_halo[2]};
+    if (c->tile < c->n_tiles - 1)
+        sd[n++] = pack ? HaloSide<R>{c->own_hi - 1, HALO_TO_RIGHT_N, HALO_TO_RIGHT, (R *)c->d_halo[1]}
+                       : HaloSide<R>{c->N - 1, HALO_TO_LEFT_N, HALO_TO_LEFT, (R *)c->d_halo[3]};
+    halo_copy<R>(c, s, sd, n, pack);
 }
 
 // This tile's boundary columns -> d_halo[0] (to the left neighbour) and
 // d_halo[1] (to the right one); d_halo[2] / d_halo[3] (from the left / right
-// neighbour) -> the ghost columns.
+// neighbour) -> the ghost columns.  Each a single launch.
 void halo_pack(gqmap_ctx *c, hipStream_t s)
 {
-    if (c->tile > 0) halo_move(c, s, c->own_lo, HALO_TO_LEFT, HALO_TO_LEFT_N, c->d_halo[0], true);
-    if (c->tile < c->n_tiles - 1) halo_move(c, s, c->own_hi - 1, HALO_TO_RIGHT, HALO_TO_RIGHT_N, c->d_halo[1], true);
+    if (c->fp32) halo_move<float>(c, s, true);
+    else halo_move<double>(c, s, true);
 }
 void halo_unpack(gqmap_ctx *c, hipStream_t s)
 {
-    if (c->tile > 0) halo_move(c, s, 0, HALO_TO_RIGHT, HALO_TO_RIGHT_N, c->d_halo[2], false);
-    if (c->tile < c->n_tiles - 1) halo_move(c, s, c->N - 1, HALO_TO_LEFT, HALO_TO_LEFT_N, c->d_halo[3], false);
+    if (c->fp32) halo_move<float>(c, s, false);
+    else halo_move<double>(c, s, false);
 }
 
 // The rest of a whole-grid iteration after k_iter: the finalize, unless the
