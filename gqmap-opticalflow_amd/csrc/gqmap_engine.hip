@@ -1273,11 +1273,12 @@ struct HaloSide {
     uint32_t planes;
     R *buf;
 };
-// Both sides of a pack or unpack in one launch: blockIdx.y picks the side
-// (the strip ends have one; nsides = 1).
+// Pack: the tile's boundary columns of the buffer the iteration just wrote
+// -> the send buffers, both sides in one launch (blockIdx.y picks the side;
+// the strip ends have one).
 template <typename R>
 __global__ void k_halo_copy(const Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL, int L,
-                            HaloSide<R> s0, HaloSide<R> s1, int to_buf)
+                            HaloSide<R> s0, HaloSide<R> s1)
 {
     if (ctl->stop) return;
     R *dst = (ctl->done & 1) ? st0 : st1;
@@ -1291,9 +1292,36 @@ __global__ void k_halo_copy(const Ctl *ctl, R *st0, R *st1, int M, int64_t MN, i
         const int64_t ql = t / M;  // qi * L + l
         const int q = (int)((planes >> (4 * (int)(ql / L))) & 15u), l = (int)(ql % L);
         R *p = dst + (int64_t)q * MNL + (int64_t)l * MN + (int64_t)col * M + m;
-        if (to_buf) buf[t] = *p;
-        else *p = buf[t];
+        buf[t] = *p;
     }
+}
+
+// A tile's ghost-column unpack and its finalize in one launch (one
+// workgroup): the received columns go into the state buffer the iteration
+// just wrote (parity read before fin_apply flips it), then the exact
+// reduction of all tiles' totals and the iteration's control step.
+template <typename R>
+__global__ __launch_bounds__(256) void k_unpack_finalize(FinParams F, R *st0, R *st1, int M, int64_t MN,
+                                                         int64_t MNL, int L, HaloSide<R> s0, HaloSide<R> s1,
+                                                         int nsides)
+{
+    Ctl *ctl = F.ctl;
+    if (ctl->stop) return;
+    R *dst = (ctl->done & 1) ? st0 : st1;
+    for (int k = 0; k < nsides; ++k) {
+        const HaloSide<R> &hs = k == 0 ? s0 : s1;
+        const int64_t n = (int64_t)hs.np * L * M;
+        for (int64_t t = threadIdx.x; t < n; t += 256) {
+            const int m = (int)(t % M);
+            const int64_t ql = t / M;
+            const int q = (int)((hs.planes >> (4 * (int)(ql / L))) & 15u), l = (int)(ql % L);
+            dst[(int64_t)q * MNL + (int64_t)l * MN + (int64_t)hs.col * M + m] = hs.buf[t];
+        }
+    }
+    __shared__ fix128 sh[256];
+    __shared__ double tot[NFIX + GQMAP_LMAX];
+    fin_reduce(F, tot, sh);  // (its barriers order every thread's parity read before fin_apply)
+    if (threadIdx.x == 0) fin_apply(F, tot);
 }
 
 template <typename R>
@@ -1760,7 +1788,7 @@ namespace {
 
 // sides: the present ones (left and/or right), one launch
 template <typename R>
-void halo_copy(gqmap_ctx *c, hipStream_t s, const HaloSide<R> *sides, int nsides, bool to_buf)
+void halo_copy(gqmap_ctx *c, hipStream_t s, const HaloSide<R> *sides, int nsides)
 {
     if (nsides == 0) return;
     int64_t n = 0;
@@ -1768,36 +1796,45 @@ void halo_copy(gqmap_ctx *c, hipStream_t s, const HaloSide<R> *sides, int nsides
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
     k_halo_copy<R><<<dim3(grid, nsides), 256, 0, s>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M,
                                                      (int64_t)c->M * c->N, c->MNL, c->L, sides[0],
-                                                     sides[nsides - 1], to_buf);
+                                                     sides[nsides - 1]);
 }
 
-// (column, planes, buffer) of the left / right side; left = the side towards tile - 1
+// This tile's boundary columns -> d_halo[0] (to the left neighbour, tile - 1)
+// and d_halo[1] (to the right one), one launch; d_halo[2] / d_halo[3] (from
+// the left / right neighbour) go into the ghost columns in
+// k_unpack_finalize.
 template <typename R>
-void halo_move(gqmap_ctx *c, hipStream_t s, bool pack)
+void halo_pack_t(gqmap_ctx *c, hipStream_t s)
 {
     HaloSide<R> sd[2];
     int n = 0;
-    if (c->tile > 0)
-        sd[n++] = pack ? HaloSide<R>{c->own_lo, HALO_TO_LEFT_N, HALO_TO_LEFT, (R *)c->d_halo[0]}
-                       : HaloSide<R>{0, HALO_TO_RIGHT_N, HALO_TO_RIGHT, (R *)c->d_halo[2]};
-    if (c->tile < c->n_tiles - 1)
-        sd[n++] = pack ? HaloSide<R>{c->own_hi - 1, HALO_TO_RIGHT_N, HALO_TO_RIGHT, (R *)c->d_halo[1]}
-                       : HaloSide<R>{c->N - 1, HALO_TO_LEFT_N, HALO_TO_LEFT, (R *)c->d_halo[3]};
-    halo_copy<R>(c, s, sd, n, pack);
+    if (c->tile > 0) sd[n++] = HaloSide<R>{c->own_lo, HALO_TO_LEFT_N, HALO_TO_LEFT, (R *)c->d_halo[0]};
+    if (c->tile < c->n_tiles - 1) sd[n++] = HaloSide<R>{c->own_hi - 1, HALO_TO_RIGHT_N, HALO_TO_RIGHT, (R *)c->d_halo[1]};
+    halo_copy<R>(c, s, sd, n);
 }
-
-// This tile's boundary columns -> d_halo[0] (to the left neighbour) and
-// d_halo[1] (to the right one); d_halo[2] / d_halo[3] (from the left / right
-// neighbour) -> the ghost columns.  Each a single launch.
 void halo_pack(gqmap_ctx *c, hipStream_t s)
 {
-    if (c->fp32) halo_move<float>(c, s, true);
-    else halo_move<double>(c, s, true);
+    if (c->fp32) halo_pack_t<float>(c, s);
+    else halo_pack_t<double>(c, s);
 }
-void halo_unpack(gqmap_ctx *c, hipStream_t s)
+
+// The received ghost columns and the finalize of a tile, one launch on the
+// tile's stream (k_unpack_finalize)
+template <typename R>
+void unpack_finalize_t(gqmap_ctx *c)
 {
-    if (c->fp32) halo_move<float>(c, s, false);
-    else halo_move<double>(c, s, false);
+    HaloSide<R> sd[2];
+    int n = 0;
+    if (c->tile > 0) sd[n++] = HaloSide<R>{0, HALO_TO_RIGHT_N, HALO_TO_RIGHT, (R *)c->d_halo[2]};
+    if (c->tile < c->n_tiles - 1) sd[n++] = HaloSide<R>{c->N - 1, HALO_TO_LEFT_N, HALO_TO_LEFT, (R *)c->d_halo[3]};
+    if (n == 0) sd[0] = HaloSide<R>{0, 0, 0u, nullptr};
+    k_unpack_finalize<R><<<1, 256, 0, c->stream>>>(fin_params(c), (R *)c->d_st[0], (R *)c->d_st[1], c->M,
+                                                   (int64_t)c->M * c->N, c->MNL, c->L, sd[0], sd[n > 0 ? n - 1 : 0], n);
+}
+void unpack_finalize(gqmap_ctx *c)
+{
+    if (c->fp32) unpack_finalize_t<float>(c);
+    else unpack_finalize_t<double>(c);
 }
 
 // The rest of a whole-grid iteration after k_iter: the finalize, unless the
@@ -1857,10 +1894,9 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     GQ_HIP(hipStreamWaitEvent(c->side, c->ev_inr, 0));
     GQ_NCCL(R->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
                          c->comm->comm, c->side));
-    halo_unpack(c, c->side);
     GQ_HIP(hipEventRecord(c->ev_xch, c->side));
     GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_xch, 0));
-    launch_finalize(c);
+    unpack_finalize(c);  // received ghost columns + finalize, one launch
     return GQMAP_OK;
 }
 
@@ -2821,8 +2857,7 @@ gqmap_status gqmap_tile_exchange_end(gqmap_ctx *c, const void *recv_left, const 
         GQ_HIP(hipMemcpyAsync(c->d_halo[3], recv_right, halo_bytes(c, 3), hipMemcpyHostToDevice, c->stream));
     GQ_HIP(hipMemcpyAsync(c->d_gathered, totals_all, sizeof(fix128) * NP * c->n_tiles, hipMemcpyHostToDevice,
                           c->stream));
-    halo_unpack(c, c->stream);
-    launch_finalize(c);
+    unpack_finalize(c);
     GQ_HIP(hipGetLastError());
     GQ_HIP(hipStreamSynchronize(c->stream));
     if (trace3) {
@@ -2895,8 +2930,7 @@ gqmap_status gqmap_tile_group_run(gqmap_ctx **tiles, int n, int n_iter, int *n_d
                                         hipMemcpyDeviceToDevice, t0->stream) != hipSuccess)
                 s = GQMAP_ERR_HIP;
         }
-        for (int t = 0; t < n; ++t) halo_unpack(tiles[t], tiles[t]->stream);
-        for (int t = 0; t < n; ++t) launch_finalize(tiles[t]);
+        for (int t = 0; t < n; ++t) unpack_finalize(tiles[t]);
         if (hipGetLastError() != hipSuccess) s = GQMAP_ERR_HIP;
         if (i % 64 == 63 && s == GQMAP_OK) {  // stop test, bounded queue depth, trace drain
             Ctl h;
