@@ -213,6 +213,7 @@ struct IterParams {
     double step0, step_decay;
     int guard;
     int64_t MNL;
+    unsigned *bar;  // k_iter_persist: barrier counters (BAR_WORDS, zero between launches)
 };
 
 // Quadrature tables are read with wave-uniform indices; routing them through
@@ -619,6 +620,34 @@ __device__ __forceinline__ bool node_interior(const IterParams<R, VT> &P, int mm
            nn + P.n_off <= P.Ng - 2;
 }
 
+// State-buffer access.  COH (the persistent small-grid kernel, whose
+// workgroups hand state to each other inside one launch): device-coherent
+// (agent-scope relaxed) loads and stores -- write-through on the producer,
+// L1 bypassed on the consumer -- so no L2 write-back / invalidate is needed
+// between its iterations.  Otherwise plain accesses (kernel boundaries order
+// them).
+#ifndef GQ_PERSIST_PLAIN  // timing experiment only (stale reads): plain state accesses in k_iter_persist
+#define GQ_PERSIST_PLAIN 0
+#endif
+#ifndef GQ_PERSIST_NOFIN  // timing experiment only (no trace / stop): the finalizer only arrives
+#define GQ_PERSIST_NOFIN 0
+#endif
+#ifndef GQ_PERSIST_SLEEP
+#define GQ_PERSIST_SLEEP 2
+#endif
+template <bool COH, typename R>
+__device__ __forceinline__ R ld_state(const R *p)
+{
+    if constexpr (COH && !GQ_PERSIST_PLAIN) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool COH, typename R>
+__device__ __forceinline__ void st_state(R *p, R v)
+{
+    if constexpr (COH && !GQ_PERSIST_PLAIN) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 // Edge job e of a lane: e = dir + 2*uv (< 4) is the node's own down / right
 // edge, e = 4 the halo edge entering the tile (top row / left column) that
 // the lane group tid / Q computes; with its operands loaded (rou plane 5+e of
@@ -629,7 +658,7 @@ struct EdgeJob {
     bool need;
     R u1, o1, p, o2, u2;
 };
-template <typename R, typename VT, int Q, int TM, int TN>
+template <typename R, typename VT, int Q, int TM, int TN, bool COH>
 __device__ __forceinline__ EdgeJob<R> edge_job(const IterParams<R, VT> &P, const R *__restrict__ src, int e,
                                                int tid, int m, int n, int m0, int n0, int64_t loff, bool inner,
                                                bool valid, R mu_u, R mu_v, R sg_u, R sg_v)
@@ -659,11 +688,11 @@ __device__ __forceinline__ EdgeJob<R> edge_job(const IterParams<R, VT> &P, const
         const int uv = jb.uv;
         const int64_t h = hm + (int64_t)M * hn + loff;
         const int64_t r = rm + (int64_t)M * rn + loff;
-        jb.u1 = own_edge ? (uv ? mu_v : mu_u) : src[h + MNL * uv];
-        jb.o1 = own_edge ? (uv ? sg_v : sg_u) : src[h + MNL * (2 + uv)];
-        jb.p = src[h + MNL * (5 + jb.dir + 2 * uv)];  // rou plane 5+e
-        jb.o2 = src[r + MNL * (2 + uv)];
-        jb.u2 = src[r + MNL * uv];
+        jb.u1 = own_edge ? (uv ? mu_v : mu_u) : ld_state<COH>(src + h + MNL * uv);
+        jb.o1 = own_edge ? (uv ? sg_v : sg_u) : ld_state<COH>(src + h + MNL * (2 + uv));
+        jb.p = ld_state<COH>(src + h + MNL * (5 + jb.dir + 2 * uv));  // rou plane 5+e
+        jb.o2 = ld_state<COH>(src + r + MNL * (2 + uv));
+        jb.u2 = ld_state<COH>(src + r + MNL * uv);
     }
     return jb;
 }
@@ -671,7 +700,7 @@ __device__ __forceinline__ EdgeJob<R> edge_job(const IterParams<R, VT> &P, const
 // The clamped ascent of one interior node from its assembled gradients
 // (gqmap_gpu_mixture.m:41-45; gqmap_ctf.m:34-35), the updated state into dst
 // and the node's exact contributions to the block sums; returns its dalpha.
-template <int ENG, typename R, typename VT>
+template <int ENG, bool COH, typename R, typename VT>
 __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__restrict__ dst, int64_t i, int m,
                                              int n, R step, R mu_u, R mu_v, R sg_u, R sg_v, R pn, const Grad<R> &nd,
                                              R gmu_u, R gmu_v, R gsg_u, R gsg_v, R eE, R eda, fix128 &fE,
@@ -681,8 +710,8 @@ __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__re
     const int64_t MNL = P.MNL, MN = (int64_t)M * P.N;
     auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
     const R nu = cl(mu_u + gmu_u * step, P.minu, P.maxu), nv = cl(mu_v + gmu_v * step, P.minv, P.maxv);
-    dst[i + MNL * 0] = nu;
-    dst[i + MNL * 1] = nv;
+    st_state<COH, R>(dst + i + MNL * 0, nu);
+    st_state<COH, R>(dst + i + MNL * 1, nv);
     if constexpr (ENG == 2) {  // AEPE of gqmap_ctf.m:38 against the updated mean
         if (P.truth) {
             const double du = P.truth[m + (int64_t)M * n] - (double)nu;
@@ -693,9 +722,9 @@ __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__re
     // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
     const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
     const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
-    dst[i + MNL * 2] = cl(sg_u + su, P.sig_lo, P.sig_hi);
-    dst[i + MNL * 3] = cl(sg_v + sv, P.sig_lo, P.sig_hi);
-    dst[i + MNL * 4] = cl(pn + nd.dp * step, -P.corr, P.corr);
+    st_state<COH, R>(dst + i + MNL * 2, cl(sg_u + su, P.sig_lo, P.sig_hi));
+    st_state<COH, R>(dst + i + MNL * 3, cl(sg_v + sv, P.sig_lo, P.sig_hi));
+    st_state<COH, R>(dst + i + MNL * 4, cl(pn + nd.dp * step, -P.corr, P.corr));
     // per-node contributions to the global sums (exact fixed point)
     const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
     const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
@@ -778,9 +807,12 @@ __device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, 
 // One tile of one iteration (absolute iteration `it`, reading state buffer
 // `parity`): node and edge gradients, neighbour scatter, clamped ascent into
 // the other buffer, and the tile's exact partial sums into partial row part_r.
-template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST>
+// Tcur: the temperature of this iteration (Ctl::T; the persistent kernel keeps
+// its own copy).  tab_ready: the LDS table is already loaded (persistent).
+template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
-                                          int part_r, TileLds<R, BLOCK / Q> &lds, int l0, int l1)
+                                          int part_r, TileLds<R, BLOCK / Q> &lds, int l0, int l1, double Tcur,
+                                          bool tab_ready)
 {
     constexpr int TPIX = BLOCK / Q;                   // nodes per tile
     constexpr int TM = tile_rows(Q), TN = TPIX / TM;  // tile rows x columns
@@ -788,7 +820,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     Ctl *ctl = P.ctl;
     const R *__restrict__ src = parity ? P.st1 : P.st0;
     R *__restrict__ dst = parity ? P.st0 : P.st1;
-    const R T = R(ctl->T);
+    const R T = R(Tcur);
     const R step = R(P.step0 / (1.0 + it / P.step_decay));
 
     const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
@@ -807,8 +839,10 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     using tab_t = std::conditional_t<TAB_LDS, const R *, ctab_t<R>>;
     tab_t tab;
     if constexpr (TAB_LDS) {
-        for (int e = threadIdx.x; e < NTAB * K2; e += BLOCK) lds.tab[e] = P.tab[e];
-        __syncthreads();
+        if (!tab_ready) {
+            for (int e = threadIdx.x; e < NTAB * K2; e += BLOCK) lds.tab[e] = P.tab[e];
+            __syncthreads();
+        }
         tab = lds.tab;
     } else {
         tab = as_const(P.tab);
@@ -832,11 +866,11 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // are read and updated by their edge jobs.  (Named scalars, not an
         // array: a select between two array elements by the run-time uv
         // below would put the array in scratch.)
-        const R mu_u = valid ? src[i] : R(0);
-        const R mu_v = valid ? src[i + MNL] : R(0);
-        const R sg_u = valid ? src[i + MNL * 2] : R(0);
-        const R sg_v = valid ? src[i + MNL * 3] : R(0);
-        const R pn = valid ? src[i + MNL * 4] : R(0);
+        const R mu_u = valid ? ld_state<COH>(src + i) : R(0);
+        const R mu_v = valid ? ld_state<COH>(src + i + MNL) : R(0);
+        const R sg_u = valid ? ld_state<COH>(src + i + MNL * 2) : R(0);
+        const R sg_v = valid ? ld_state<COH>(src + i + MNL * 3) : R(0);
+        const R pn = valid ? ld_state<COH>(src + i + MNL * 4) : R(0);
         Grad<R> nd{};
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R eE = 0, eda = 0;                                     // sum over the 4 edges
@@ -880,7 +914,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // job e+1's operands before computing job e
         constexpr bool PREFETCH = Q >= GQ_PREFETCH_MIN_Q;
         auto job_at = [&](int e) {
-            return edge_job<R, VT, Q, TM, TN>(P, src, e, tid, m, n, m0, n0, MN * l, inner, valid, mu_u, mu_v,
+            return edge_job<R, VT, Q, TM, TN, COH>(P, src, e, tid, m, n, m0, n0, MN * l, inner, valid, mu_u, mu_v,
                                                 sg_u, sg_v);
         };
         EdgeJob<R> next{};
@@ -911,7 +945,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                 // the edge owns its correlation: clamped ascent right here
                 // (gqmap_gpu_mixture.m:46), nothing else reads drou
                 if (own_edge && inner && lead)
-                    dst[i + MNL * (5 + e)] = fmin(fmax(jb.p + g.dp * step, -P.corr), P.corr);
+                    st_state<COH, R>(dst + i + MNL * (5 + e), fmin(fmax(jb.p + g.dp * step, -P.corr), P.corr));
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
@@ -938,7 +972,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][pix]) + in_left[1][0][pix];
             const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][pix]) + in_left[0][1][pix];
             const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
-            fda = node_apply<ENG>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u, gsg_v,
+            fda = node_apply<ENG, COH>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u, gsg_v,
                                   eE, eda, fE, fmu, fsg, fae, nonfinite);
         }
         if (P.L > 1) {  // dalpha(l): only consumed by the alpha update
@@ -1009,9 +1043,9 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
     } else if (edge_first)
-        iter_tile<R, VT, ENG, Q, true>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, true>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1, ctl->T, false);
     else
-        iter_tile<R, VT, ENG, Q, false>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1);
+        iter_tile<R, VT, ENG, Q, false>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1, ctl->T, false);
 #if GQ_TIMELINE
     __syncthreads();
     TL_STAMP(0, tl0);
@@ -1088,26 +1122,20 @@ struct WnLds {
     R tab[NTAB * TS];
 };
 
-template <typename R, typename VT, int ENG>
-__global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
+// One tile (WN_TM x 1 nodes) of one iteration; block b's partial row part_r.
+// copy_tab: load the quadrature table into LDS first (the persistent kernel
+// loads it once).
+template <typename R, typename VT, int ENG, bool COH>
+__device__ __forceinline__ void wn_tile(const IterParams<R, VT> &P, int tile, int it, int parity, double Tcur,
+                                        int part_r, WnLds<R> &lds, bool copy_tab)
 {
     Ctl *ctl = P.ctl;
-    if (ctl->stop) return;
-#if GQ_TIMELINE
-    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    const int nb = P.seg_n[0] + P.seg_n[1];
-    const int b = blockIdx.x;
-    const int tl = tile_of_block(b, nb, 1, P.cu_slots);
-    const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
-    __shared__ WnLds<R> lds;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int grp = lane >> 4, gl = lane & 15;  // 16-lane group of the edge jobs
     const int K2 = P.K2;
-    const int it = ctl->it, parity = ctl->done & 1;
     const R *__restrict__ src = parity ? P.st1 : P.st0;
     R *__restrict__ dst = parity ? P.st0 : P.st1;
-    const R T = R(ctl->T);
+    const R T = R(Tcur);
     const R step = R(P.step0 / (1.0 + it / P.step_decay));
     const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
     const int m = tm * WN_TM + wave, n = tn;
@@ -1129,12 +1157,15 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
         // jobs, loaded before the table copy's barrier
         R mu_u = 0, mu_v = 0, sg_u = 0, sg_v = 0, pn = 0, p1 = 0, u2 = 0, o2 = 0, p2 = 0, hu = 0, ho = 0;
         if (inner) {
-            mu_u = src[i]; mu_v = src[i + MNL]; sg_u = src[i + MNL * 2]; sg_v = src[i + MNL * 3];
-            pn = src[i + MNL * 4];
-            p1 = src[i + MNL * (5 + grp)]; u2 = src[r + MNL * uv]; o2 = src[r + MNL * (2 + uv)];
-            p2 = src[h + MNL * (5 + grp)]; hu = src[h + MNL * uv]; ho = src[h + MNL * (2 + uv)];
+            mu_u = ld_state<COH>(src + i); mu_v = ld_state<COH>(src + i + MNL);
+            sg_u = ld_state<COH>(src + i + MNL * 2); sg_v = ld_state<COH>(src + i + MNL * 3);
+            pn = ld_state<COH>(src + i + MNL * 4);
+            p1 = ld_state<COH>(src + i + MNL * (5 + grp)); u2 = ld_state<COH>(src + r + MNL * uv);
+            o2 = ld_state<COH>(src + r + MNL * (2 + uv));
+            p2 = ld_state<COH>(src + h + MNL * (5 + grp)); hu = ld_state<COH>(src + h + MNL * uv);
+            ho = ld_state<COH>(src + h + MNL * (2 + uv));
         }
-        if (l == 0) {
+        if (l == 0 && copy_tab) {
             for (int e = tid; e < NTAB * K2; e += WN_THREADS) lds.tab[e] = P.tab[e];
             __syncthreads();
             TL_STAMP(1, __builtin_amdgcn_s_memrealtime());
@@ -1153,7 +1184,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
             Sums<R> S1 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c1);
             S1 = lane_combine<16>(S1);
             const Grad<R> g1 = edge_epi(S1, c1, P.lams, P.guard != 0, T, a, own_o, o2, p1, ENG == 2);
-            if (gl == 0) dst[i + MNL * (5 + grp)] = fmin(fmax(p1 + g1.dp * step, -P.corr), P.corr);
+            if (gl == 0) st_state<COH, R>(dst + i + MNL * (5 + grp), fmin(fmax(p1 + g1.dp * step, -P.corr), P.corr));
             // round 2: the edge entering from the head node h (its edge grp)
             const EdgeCoef<R> c2 = edge_coef(hu, own_u, ho, own_o, p2);
             Sums<R> S2 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c2);
@@ -1183,7 +1214,7 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
                 const R gmu_v = ((nd.du2 + sum_mu1) + up[1][0]) + left[1][0];
                 const R gsg_u = ((nd.do1 + sum_sg0) + up[0][1]) + left[0][1];
                 const R gsg_v = ((nd.do2 + sum_sg1) + up[1][1]) + left[1][1];
-                fda = node_apply<ENG>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u,
+                fda = node_apply<ENG, COH>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u,
                                       gsg_v, eE, eda, fE, fmu, fsg, fae, nonfinite);
             }
         }
@@ -1208,13 +1239,204 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
         if (P.fused || P.tile_acc) {
             if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
         } else {
-            store_part_agent(P.partials, P.fin.nblocks, P.part_off + b, tid, v);
+            store_part_agent(P.partials, P.fin.nblocks, part_r, tid, v);
         }
     }
+}
+
+template <typename R, typename VT, int ENG>
+__global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
+{
+    Ctl *ctl = P.ctl;
+    if (ctl->stop) return;
+#if GQ_TIMELINE
+    const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int nb = P.seg_n[0] + P.seg_n[1];
+    const int b = blockIdx.x;
+    const int tl = tile_of_block(b, nb, 1, P.cu_slots);
+    const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
+    __shared__ WnLds<R> lds;
+    wn_tile<R, VT, ENG, false>(P, tile, ctl->it, ctl->done & 1, ctl->T, P.part_off + b, lds, true);
     TL_STAMP(0, tl0);
     TL_STAMP(4, __builtin_amdgcn_s_memrealtime());
     if (P.fused) fused_finalize_tail(P.fin);
     else if (P.tile_acc) tile_totals_tail(P.fin, P.ticket_total, P.tile_totals);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent small-grid kernel (ctf engine, L = 1, every workgroup
+// co-resident): one launch runs a chunk of iterations.  Workgroups 0..G-1 own
+// one tile each (the k_iter / k_iter_wn tiles, same arithmetic, same bits);
+// workgroup G is the finalizer.  Iteration j's state goes from one workgroup
+// to its neighbours through device-coherent stores and loads (ld_state /
+// st_state), its exact partial sums through partial rows (j & 1) * G + b,
+// and a grid barrier (per-XCD-slot arrival counters, polled together by one
+// wave) separates iteration j from j + 1.
+//
+// Nothing of the next iteration depends on the finalize step when L = 1
+// except the stop rule: alpha is constant, the step size and the temperature
+// decay depend only on the iteration number (each workgroup keeps its own T,
+// updated as fin_apply updates Ctl::T).  So the finalizer reduces iteration
+// j - 1 while the tiles compute iteration j; iteration j is speculative until
+// finalize(j - 1) has run.  Before iteration j + 1 (after barrier j, by which
+// the finalizer has finished finalize(j - 1)) every workgroup reads the stop
+// flag: if iteration j - 1 met the stop rule, iteration j is discarded (it
+// wrote the buffer that held state j - 2; state j - 1 is untouched and
+// Ctl::done still points at it) and everyone exits.  This replaces per
+// iteration: the launch gap, the LDS table copy and the serial fused finalize
+// of the last workgroup.
+// ---------------------------------------------------------------------------
+constexpr int BAR_LINE = 32;  // unsigned words per 128-byte line: one counter per line
+// BAR_STOP: 1 + the launch-local index of the iteration that met the stop
+// rule (0: none).  Per iteration, not a flag: the finalizer may already be
+// writing finalize(j - 1)'s verdict while a slow workgroup still reads
+// finalize(j - 2)'s after barrier j - 1.
+constexpr int BAR_EXIT = 8 * BAR_LINE, BAR_FAIL = 9 * BAR_LINE, BAR_STOP = 10 * BAR_LINE, BAR_WORDS = 11 * BAR_LINE;
+constexpr unsigned BAR_SPIN_LIMIT = 1u << 21;  // polls (~1 us each) before a barrier gives up
+
+// Arrival: every wave's stores (state, partial row) have completed, then one
+// lane adds to the counter of its slot (blockIdx & 7: blocks of one XCD).
+__device__ __forceinline__ void pbar_arrive(unsigned *bar)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(bar + (blockIdx.x & 7) * BAR_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait for barrier phase j (0-based) over nblk workgroups: wave 0 polls the 8
+// slot counters (slot x receives (nblk - x + 7) / 8 arrivals per phase) and
+// the failure word together.  Then the stop word: iteration j + 1 runs only
+// if no iteration up to j - 1 met the stop rule (the finalizer judged those
+// before its arrival at barrier j).  Returns true when the caller should go
+// on: the barrier completed and no stop.  A spin that exceeds BAR_SPIN_LIMIT (the
+// grid was not co-resident) raises the failure word and returns false; the
+// host reports it.
+__device__ __forceinline__ bool pbar_wait(unsigned *bar, int j, int nblk, int *sh_flag)
+{
+    if (threadIdx.x < 64) {
+        const int x = threadIdx.x;
+        const unsigned need = x < 8 ? (unsigned)((nblk - x + 7) >> 3) * (unsigned)(j + 1) : 0u;
+        unsigned spins = 0;
+        int go = 1;
+        while (true) {
+            unsigned v = 0xffffffffu, f = 0;
+            if (x < 8) v = __hip_atomic_load(bar + x * BAR_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (x == 8) f = __hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__any(f != 0)) { go = 0; break; }
+            if (__all(v >= need)) break;
+            if (++spins > BAR_SPIN_LIMIT) {
+                if (x == 0) __hip_atomic_store(bar + BAR_FAIL, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                go = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(GQ_PERSIST_SLEEP);
+        }
+        if (x == 0) {
+            if (go) {
+                const unsigned st = __hip_atomic_load(bar + BAR_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (st != 0 && (int)st <= j) go = 0;  // iteration st - 1 <= j - 1 stopped the run
+            }
+            *sh_flag = go;
+        }
+    }
+    __syncthreads();
+    return *sh_flag != 0;
+}
+
+// Exit: the last workgroup out (all others are past their last poll) clears
+// the counters for the next launch (the failure word stays for the host).
+__device__ __forceinline__ void pbar_exit(unsigned *bar, int nblk)
+{
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(bar + BAR_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == (unsigned)nblk - 1) {
+            for (int x = 0; x < 8; ++x)
+                __hip_atomic_store(bar + x * BAR_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bar + BAR_STOP, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(bar + BAR_EXIT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Finalizer: exact reduction of partial rows [row0, row0 + rows) (L = 1: the
+// NFIX fixed sums; integer adds, any order) into tot[].
+__device__ void pfin_reduce(const FinParams &F, int row0, int rows, double *tot, fix128 (*sh)[8])
+{
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    fix128 v[NFIX] = {};
+    for (int r = tid; r < rows; r += blockDim.x)
+#pragma unroll
+        for (int q = 0; q < NFIX; ++q) v[q] += load_part_agent(F.partials, F.nblocks, row0 + r, q);
+#pragma unroll
+    for (int q = 0; q < NFIX; ++q) {
+        const fix128 w = wave_sum_fix(v[q]);
+        if (lane == 0) sh[q][wave] = w;
+    }
+    __syncthreads();
+    if (tid < NFIX) {
+        fix128 t = 0;
+        for (int w = 0; w < nw; ++w) t += sh[tid][w];
+        tot[tid] = from_fix(t);
+    }
+    __syncthreads();
+}
+
+template <typename R, typename VT, int ENG, int Q>
+__global__ __launch_bounds__(Q == 64 ? WN_THREADS : BLOCK, Q == 64 ? 1 : min_waves(ENG, Q))
+void k_iter_persist(IterParams<R, VT> P, int n_iter)
+{
+    Ctl *ctl = P.ctl;
+    // nothing writes Ctl before the first barrier, which every workgroup
+    // reaches only after these reads: all workgroups see the same values
+    if (ctl->stop) return;
+    const int nblk = gridDim.x, G = nblk - 1, b = blockIdx.x;
+    const int it0 = ctl->it, done0 = ctl->done;
+    double T = ctl->T;
+    unsigned *bar = P.bar;
+    __shared__ int sh_flag;
+    if (b == G) {  // finalizer: finalize(j - 1) during iteration j
+        __shared__ fix128 fsh[NFIX][8];
+        __shared__ double tot[NFIX];
+        for (int j = 0; j <= n_iter; ++j) {
+            if (j > 0) {
+                if (!pbar_wait(bar, j - 1, nblk, &sh_flag)) break;
+                if (GQ_PERSIST_NOFIN) { if (j < n_iter) pbar_arrive(bar); continue; }
+                pfin_reduce(P.fin, ((j - 1) & 1) * G, G, tot, fsh);
+                if (threadIdx.x == 0) {
+                    fin_apply(P.fin, tot);
+                    // the verdict travels device-coherent (read by pbar_wait)
+                    if (ctl->stop)
+                        __hip_atomic_store(bar + BAR_STOP, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (j < n_iter) pbar_arrive(bar);
+        }
+        pbar_exit(bar, nblk);
+        return;
+    }
+    const int tile = tile_of_block(b, G, Q == 64 ? 1 : P.cu_group, P.cu_slots);
+    const bool edge_first = GQ_PHASE_MIX && Q != 64 && (((b >> 3) / P.cu_slots) & 1);
+    for (int j = 0; j < n_iter; ++j) {
+        if (j > 0 && !pbar_wait(bar, j - 1, nblk, &sh_flag)) break;
+        const int it = it0 + j, parity = (done0 + j) & 1, part_r = ((j & 1) * G) + b;
+        if constexpr (Q == 64) {
+            __shared__ WnLds<R> lds_wn;
+            wn_tile<R, VT, ENG, true>(P, tile, it, parity, T, part_r, lds_wn, j == 0);
+        } else {
+            __shared__ TileLds<R, BLOCK / Q> lds;
+            if (edge_first)
+                iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, parity, part_r, lds, 0, P.L, T, j > 0);
+            else
+                iter_tile<R, VT, ENG, Q, false, true>(P, tile, it, parity, part_r, lds, 0, P.L, T, j > 0);
+        }
+        pbar_arrive(bar);
+        // fin_apply's temperature decay after iteration it (gqmap_gpuSuper_mix_entropy.m:72)
+        if (P.fin.t_decay_every > 0 && it % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
+    }
+    pbar_exit(bar, nblk);
 }
 
 __global__ __launch_bounds__(256) void k_finalize(FinParams F)
@@ -1429,7 +1651,8 @@ struct gqmap_ctx {
     size_t rsz = 8;
     void *d_VV = nullptr, *d_I1 = nullptr, *d_st[2] = {nullptr, nullptr}, *d_tab = nullptr;
     Ctl *d_ctl = nullptr;
-    fix128 *d_partials = nullptr;
+    fix128 *d_partials = nullptr;  // 2 x nblocks rows (k_iter_persist alternates halves)
+    unsigned *d_bar = nullptr;      // k_iter_persist barrier counters (BAR_WORDS)
     double *d_trace = nullptr;
     double *d_truth = nullptr;  // gqmap_set_truth: M x N x 2 (ctf engine)
     size_t truth_elems = 0;     // doubles d_truth was allocated for
@@ -1527,7 +1750,7 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     }
     if (c->d_partials) (void)hipFree(c->d_partials);
     c->d_partials = nullptr;
-    GQ_HIP(hipMalloc((void **)&c->d_partials, sizeof(fix128) * (size_t)c->nblocks * (NFIX + c->L) + 64));
+    GQ_HIP(hipMalloc((void **)&c->d_partials, sizeof(fix128) * (size_t)2 * c->nblocks * (NFIX + c->L) + 64));
     return GQMAP_OK;
 }
 
@@ -1580,6 +1803,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.tile_totals = c->d_gathered ? c->d_gathered + (size_t)c->tile * (NFIX + c->L) : nullptr;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
+    P.bar = c->d_bar;
     return P;
 }
 
@@ -1726,6 +1950,75 @@ void launch_iter(gqmap_ctx *c, const TileSegs *sg = nullptr)
 
 
 void launch_finalize(gqmap_ctx *c) { k_finalize<<<1, 256, 0, c->stream>>>(fin_params(c)); }
+
+// ---- persistent small-grid launches (k_iter_persist) ------------------------
+// Whole-grid ctf contexts with L = 1 and Q >= 8 (grids below 2^13 nodes)
+// whose tiles plus the finalizer fit the device's resident workgroups
+// (GQMAP_NO_PERSIST=1: one launch per iteration instead).
+template <typename R, typename VT, int Q>
+int persist_capacity()
+{
+    static int cap = -1;
+    if (cap < 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_iter_persist<R, VT, 2, Q>,
+                                                         Q == 64 ? WN_THREADS : BLOCK, 0) != hipSuccess)
+            per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+        // a 5-wave k_iter_wn workgroup: one per CU (the occupancy API answered
+        // 2 for the 165-VGPR fp32 instantiation, but 265 workgroups on 256 CUs
+        // were not co-resident: the barrier timed out); 4-wave workgroups
+        // take one wave slot per SIMD each, as the API counts them
+        if (Q == 64) per_cu = std::min(per_cu, 1);
+        cap = std::max(0, per_cu) * std::max(0, cus);
+    }
+    return cap;
+}
+
+template <typename R, typename VT, int Q>
+bool launch_persist_q(gqmap_ctx *c, int n, bool dry)
+{
+    const int G = c->nblocks;
+    if (G + 1 > persist_capacity<R, VT, Q>()) return false;
+    if (dry) return true;
+    IterParams<R, VT> P = iter_params<R, VT>(c);
+    P.fused = 0;
+    P.tile_acc = 0;
+    P.fin.nblocks = 2 * G;  // partial row stride: iteration j writes rows (j & 1) * G + b
+    const int threads = Q == 64 ? WN_THREADS : BLOCK;
+    static const int2 shape = kernel_shape(k_iter_persist<R, VT, 2, Q>);
+    P.cu_group = Q == 64 ? 1 : shape.x;
+    P.cu_slots = std::max(1, shape.y / 8);
+    k_iter_persist<R, VT, 2, Q><<<G + 1, threads, 0, c->stream>>>(P, n);
+    return true;
+}
+
+template <typename R, typename VT>
+bool launch_persist_t(gqmap_ctx *c, int n, bool dry)
+{
+    // not Q = 4 (120x160): 57.3 vs 48.8 us/it measured (profiles/r03_persist_levels.txt)
+    switch (c->split) {
+    case 8: return launch_persist_q<R, VT, 8>(c, n, dry);
+    case 16: return launch_persist_q<R, VT, 16>(c, n, dry);
+    case 64: return launch_persist_q<R, VT, 64>(c, n, dry);
+    default: return false;
+    }
+}
+
+// n iterations as one k_iter_persist launch when the context qualifies;
+// dry: only the check
+bool launch_persist(gqmap_ctx *c, int n, bool dry = false)
+{
+    static const bool off = std::getenv("GQMAP_NO_PERSIST") != nullptr;
+    if (off || c->opt.engine != GQMAP_ENGINE_CTF || c->L != 1 || c->n_tiles != 1 || c->comm || c->nranks != 0 ||
+        !fused_finalize(c) || n < 1)
+        return false;
+    if (c->fp32) return launch_persist_t<float, float>(c, n, dry);
+    if (c->vv32) return launch_persist_t<double, vvs_t>(c, n, dry);
+    return launch_persist_t<double, double>(c, n, dry);
+}
 
 // ---- RCCL, resolved at first use from librccl.so.1 (the copy torch has
 // already loaded, when it has) so the library itself carries no link-time
@@ -1907,6 +2200,33 @@ gqmap_status launch_step(gqmap_ctx *c)
     return launch_tail(c);
 }
 
+// n iterations: one persistent launch for small ctf grids, else n steps
+gqmap_status launch_steps(gqmap_ctx *c, int n)
+{
+    if (launch_persist(c, n)) return GQMAP_OK;
+    gqmap_status st = GQMAP_OK;
+    for (int i = 0; i < n && st == GQMAP_OK; ++i) st = launch_step(c);
+    return st;
+}
+
+// A persistent launch whose grid barrier gave up (workgroups not all
+// resident, e.g. another kernel holding CUs) leaves the failure word set.
+gqmap_status check_persist(gqmap_ctx *c)
+{
+    if (!launch_persist(c, 1, true)) return GQMAP_OK;
+    unsigned f = 0;
+    GQ_HIP(hipMemcpyAsync(&f, c->d_bar + BAR_FAIL, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    if (f != 0) {
+        GQ_HIP(hipMemsetAsync(c->d_bar, 0, sizeof(unsigned) * BAR_WORDS, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+        set_error("persistent iteration kernel: grid barrier timed out (%d workgroups not co-resident)",
+                  c->nblocks + 1);
+        return GQMAP_ERR_HIP;
+    }
+    return GQMAP_OK;
+}
+
 gqmap_status upload_ctl(gqmap_ctx *c, int it, double T, const double *w, const double *alpha)
 {
     Ctl h{};
@@ -1933,10 +2253,10 @@ gqmap_status read_ctl(gqmap_ctx *c, Ctl *h)
 gqmap_status ensure_graph(gqmap_ctx *c)
 {
     if (c->graph) return GQMAP_OK;
+    (void)launch_persist(c, GRAPH_CHUNK, true);  // occupancy query outside the capture
     hipGraph_t g;
     GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    gqmap_status st = GQMAP_OK;
-    for (int i = 0; i < GRAPH_CHUNK && st == GQMAP_OK; ++i) st = launch_step(c);
+    gqmap_status st = launch_steps(c, GRAPH_CHUNK);
     hipError_t ec = hipStreamEndCapture(c->stream, &g);
     if (st != GQMAP_OK) {
         if (ec == hipSuccess) (void)hipGraphDestroy(g);
@@ -2252,9 +2572,16 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
     }
     if (hipMalloc(&c->d_tab, NTAB * TS * c->rsz) != hipSuccess ||
         hipMalloc((void **)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
-        hipMalloc((void **)&c->d_trace, sizeof(double) * TRACE_W * TRACE_CAP) != hipSuccess) {
+        hipMalloc((void **)&c->d_trace, sizeof(double) * TRACE_W * TRACE_CAP) != hipSuccess ||
+        hipMalloc((void **)&c->d_bar, sizeof(unsigned) * BAR_WORDS) != hipSuccess) {
         set_error("device allocation failed");
         return fail(GQMAP_ERR_OUT_OF_MEMORY);
+    }
+    // synchronous: a pyramid level adopts another stream right after creation
+    if (hipMemsetAsync(c->d_bar, 0, sizeof(unsigned) * BAR_WORDS, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        set_error("hipMemsetAsync failed");
+        return fail(GQMAP_ERR_HIP);
     }
     if ((st = upload(c, c->d_tab, c->tab_host, NTAB * TS)) != GQMAP_OK) return fail(st);
     *out = c;
@@ -2486,11 +2813,11 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
                 left -= GRAPH_CHUNK;
             }
         }
-        for (; left > 0; --left)
-            if ((s = launch_step(c)) != GQMAP_OK) return s;
+        if (left > 0 && (s = launch_steps(c, left)) != GQMAP_OK) return s;
         GQ_HIP(hipGetLastError());
         Ctl h;
         if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+        if ((s = check_persist(c)) != GQMAP_OK) return s;
         const int ran = h.it - (h0.it + total);
         if ((s = fetch_trace(c, h0.it + total, ran, trace ? trace + 3 * total : nullptr,
                              aepe ? aepe + total : nullptr)) != GQMAP_OK)
@@ -2966,7 +3293,7 @@ void gqmap_destroy(gqmap_ctx *c)
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace,
-                    c->d_truth};
+                    c->d_truth, (void *)c->d_bar};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
