@@ -573,22 +573,31 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
 // (two 16-row columns per wave), 8 x 8, 4 x 4; lanes are m-fastest.
 // Q = 64 (k_iter_wn): one wave per node, WN_TM waves per workgroup, tiles of
 // WN_TM x 1 nodes.
+// Q = 0 (kernel shape only): the role split -- Q = 1 arithmetic on 16 x 8
+// tiles, lanes 0-127 (waves 0-1) run the node phase, lanes 128-255 (waves
+// 2-3) the edge phase of the same nodes, side by side (iter_tile).
 constexpr int WN_TM = 5;
+constexpr int tile_pix(int q) { return q == 0 ? BLOCK / 2 : q == 64 ? WN_TM : BLOCK / q; }
 constexpr int tile_rows(int q) { return q <= 2 ? 16 : q <= 8 ? 8 : q == 64 ? WN_TM : 4; }
-constexpr int tile_cols(int q) { return q == 64 ? 1 : BLOCK / q / tile_rows(q); }
+constexpr int tile_cols(int q) { return q == 64 ? 1 : tile_pix(q) / tile_rows(q); }
+constexpr int arith_q(int q) { return q == 0 ? 1 : q; }  // lanes per node of the arithmetic
 
 // LDS of one tile: in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n);
 // in_left: from (m,n-1); red: per-wave partial sums.  Declared by the kernels
 // (one copy whatever the number of iter_tile instantiations).
-template <typename R, int TPIX>
+template <typename R, int TPIX, bool TAB, bool RS>
 struct TileLds {
     R in_up[2][2][TPIX];
     R in_left[2][2][TPIX];
     fix128 red[GQMAP_LMAX + NFIX][4];
     // Q > 1: the quadrature table, so lane-varying table reads are LDS reads
     // (with Q lanes per node the index k differs across a wave's lanes)
-    R tab[TPIX < BLOCK && GQ_TAB_LDS ? NTAB * TS : 1];
+    R tab[TAB ? NTAB * TS : 1];
+    // role split: the node phase's gradient (du1, du2, do1, do2, dp, E, da)
+    R nd[RS ? 7 : 1][RS ? TPIX : 1];
 };
+template <typename R, int Q>
+using TileLdsQ = TileLds<R, tile_pix(Q), (Q > 1 && GQ_TAB_LDS), Q == 0>;
 
 #ifndef GQ_TIMELINE
 #define GQ_TIMELINE 0
@@ -811,10 +820,12 @@ __device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, 
 // its own copy).  tab_ready: the LDS table is already loaded (persistent).
 template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
-                                          int part_r, TileLds<R, BLOCK / Q> &lds, int l0, int l1, double Tcur,
+                                          int part_r, TileLdsQ<R, Q> &lds, int l0, int l1, double Tcur,
                                           bool tab_ready)
 {
-    constexpr int TPIX = BLOCK / Q;                   // nodes per tile
+    constexpr bool RS = Q == 0;                       // role split (node / edge waves)
+    constexpr int QA = arith_q(Q);                    // lanes per node of the arithmetic
+    constexpr int TPIX = tile_pix(Q);                 // nodes per tile
     constexpr int TM = tile_rows(Q), TN = TPIX / TM;  // tile rows x columns
     static_assert(TM * TN == TPIX, "tile");
     Ctl *ctl = P.ctl;
@@ -825,7 +836,11 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 
     const int tm = tile % P.tiles_m, tn = tile / P.tiles_m;
     const int tid = threadIdx.x;
-    const int pix = tid / Q, kj = tid % Q;  // node within the tile, lane within the node
+    // role split: lanes [0, TPIX) the node phase, [TPIX, 2 TPIX) the edge phase
+    // of the same TPIX nodes (wave-uniform roles)
+    const int rtid = RS ? tid % TPIX : tid;
+    const bool do_node = !RS || tid < TPIX, do_edge = !RS || tid >= TPIX;
+    const int pix = rtid / QA, kj = rtid % QA;  // node within the tile, lane within the node
     const int lm = pix % TM, ln = pix / TM;
     const int m0 = tm * TM, n0 = tn * TN;
     const int m = m0 + lm, n = n0 + ln;
@@ -835,7 +850,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     const bool inner = valid && node_interior(P, m, n);
     const bool lead = kj == 0;  // the lane that owns the node's outputs
     const int K2 = P.K2;
-    constexpr bool TAB_LDS = Q > 1 && GQ_TAB_LDS;
+    constexpr bool TAB_LDS = QA > 1 && GQ_TAB_LDS;
     using tab_t = std::conditional_t<TAB_LDS, const R *, ctab_t<R>>;
     tab_t tab;
     if constexpr (TAB_LDS) {
@@ -856,8 +871,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     int nonfinite = 0;
     const int wave = tid >> 6, lane = tid & 63;
     // halo: 2*(TN+TM) edges (top row and left column, u and v) x Q lanes
-    constexpr int HALO_LANES = 2 * (TN + TM) * Q;
-    const bool halo_lane = tid < HALO_LANES;
+    constexpr int HALO_LANES = 2 * (TN + TM) * QA;
+    const bool halo_lane = rtid < HALO_LANES;
 
     for (int l = l0; l < l1; ++l) {
         const R a = R(ctl->alpha[l]);
@@ -882,6 +897,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 #pragma unroll
         for (int ph = 0; ph < 2; ++ph) {
         if ((ph == 0) != EDGE_FIRST) {
+        if (do_node) {
         NodeCoef<R> c{};
         if (inner) c = node_coef(sg_u, sg_v, pn);
         // single-scale engine: when no sample of any node of the wave can be
@@ -891,14 +907,19 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         const bool fast = ENG == 0 && __all(!inner || node_unclamped(c, mu_u, mu_v, m, n + P.n_off, P.Mo, P.No,
                                                                      P.gh_xmax, R(ENG == 2 ? CTF_MARGIN : 0.0)));
         if (inner) {
-            Sums<R> S = fast ? node_sums<ENG, false>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
+            Sums<R> S = fast ? node_sums<ENG, false>(tab, kj, K2, QA, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
                                                      mu_u, mu_v, m, n + P.n_off)
-                             : node_sums<ENG, true>(tab, kj, K2, Q, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
+                             : node_sums<ENG, true>(tab, kj, K2, QA, P.VV, P.I1, P.M2, P.Mo, P.No, P.epsn, c,
                                                     mu_u, mu_v, m, n + P.n_off);
-            if (Q > 1) S = lane_combine<Q>(S);
+            if (QA > 1) S = lane_combine<QA>(S);
             nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, sg_u, sg_v, pn, ENG == 2);
+            if constexpr (RS) {  // to the edge lane of the same node
+                lds.nd[0][pix] = nd.du1; lds.nd[1][pix] = nd.du2; lds.nd[2][pix] = nd.do1;
+                lds.nd[3][pix] = nd.do2; lds.nd[4][pix] = nd.dp; lds.nd[5][pix] = nd.E; lds.nd[6][pix] = nd.da;
+            }
         }
-        } else {
+        }
+        } else if (do_edge) {
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
         // edges, then job 4 on the halo lanes: the edges entering the tile from
         // the row above / the column to the left.  One edge body, streamed into
@@ -908,13 +929,13 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // nothing wave-wide runs inside a job: the only cross-lane op is
         // lane_combine<Q>, an xor butterfly inside one node's Q adjacent
         // lanes, and a node's lanes are all halo lanes or none (asserted).
-        static_assert(HALO_LANES % Q == 0, "a node's lanes share their job count");
+        static_assert(HALO_LANES % QA == 0, "a node's lanes share their job count");
         const int njobs = halo_lane ? 5 : 4;
         // Q >= 4 (small grids, about one wave per SIMD: latency-bound) loads
         // job e+1's operands before computing job e
-        constexpr bool PREFETCH = Q >= GQ_PREFETCH_MIN_Q;
+        constexpr bool PREFETCH = QA >= GQ_PREFETCH_MIN_Q;
         auto job_at = [&](int e) {
-            return edge_job<R, VT, Q, TM, TN, COH>(P, src, e, tid, m, n, m0, n0, MN * l, inner, valid, mu_u, mu_v,
+            return edge_job<R, VT, QA, TM, TN, COH>(P, src, e, rtid, m, n, m0, n0, MN * l, inner, valid, mu_u, mu_v,
                                                 sg_u, sg_v);
         };
         EdgeJob<R> next{};
@@ -922,7 +943,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         // Q >= 4 single-pixel engines: a constant trip count, fully unrolled
         // (independent jobs overlap; ctf 30x40 30.0 -> 28.8 us/it; not the
         // super engine, which it would push past 256 VGPRs: C4 355 -> 407)
-        constexpr bool JOBS_UNROLLED = Q >= GQ_UNROLL_MIN_Q && ENG != 1;
+        constexpr bool JOBS_UNROLLED = QA >= GQ_UNROLL_MIN_Q && ENG != 1;
         constexpr int JOB_UNROLL = JOBS_UNROLLED ? 5 : 1;
 #pragma unroll JOB_UNROLL
         for (int e = 0; e < (JOBS_UNROLLED ? 5 : njobs); ++e) {
@@ -939,8 +960,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             Grad<R> g{};
             if (jb.need) {
                 const EdgeCoef<R> c = edge_coef(jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
-                Sums<R> S = edge_sums_dev(tab, kj, K2, Q, P.epsn, c);
-                if (Q > 1) S = lane_combine<Q>(S);
+                Sums<R> S = edge_sums_dev(tab, kj, K2, QA, P.epsn, c);
+                if (QA > 1) S = lane_combine<QA>(S);
                 g = edge_epi(S, c, P.lams, P.guard != 0, T, a, jb.o1, jb.o2, jb.p, ENG == 2);
                 // the edge owns its correlation: clamped ascent right here
                 // (gqmap_gpu_mixture.m:46), nothing else reads drou
@@ -955,7 +976,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                 // neighbour share: (m+1,n) reads in_up, (m,n+1) reads in_left
                 if (lead && dir == 0 && lm + 1 < TM) { in_up[uv][0][pix + 1] = g.du2; in_up[uv][1][pix + 1] = g.do2; }
                 if (lead && dir == 1 && ln + 1 < TN) { in_left[uv][0][pix + TM] = g.du2; in_left[uv][1][pix + TM] = g.do2; }
-            } else if (tid % Q == 0) {
+            } else if (rtid % QA == 0) {
                 if (dir == 0) { in_up[uv][0][hr * TM] = g.du2; in_up[uv][1][hr * TM] = g.do2; }
                 else          { in_left[uv][0][hr] = g.du2; in_left[uv][1][hr] = g.do2; }
             }
@@ -966,7 +987,11 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         __syncthreads();
         TL_STAMP(2, __builtin_amdgcn_s_memrealtime());
         fix128 fda = 0;
-        if (inner && lead) {
+        if (inner && lead && do_edge) {
+            if constexpr (RS) {
+                nd.du1 = lds.nd[0][pix]; nd.du2 = lds.nd[1][pix]; nd.do1 = lds.nd[2][pix];
+                nd.do2 = lds.nd[3][pix]; nd.dp = lds.nd[4][pix]; nd.E = lds.nd[5][pix]; nd.da = lds.nd[6][pix];
+            }
             // dmuu = dmuu + sum(dmu1(:,:,:,:,1),4) + circshift(dmu2(..1,1),1) + circshift(dmu2(..2,1),1,2)
             const R gmu_u = ((nd.du1 + sum_mu0) + in_up[0][0][pix]) + in_left[0][0][pix];
             const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][pix]) + in_left[1][0][pix];
@@ -1038,7 +1063,7 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     // XCD (see tile_of_block): alternate the phase order among them.  Not
     // for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
     const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
-    __shared__ TileLds<R, BLOCK / Q> lds;
+    __shared__ TileLdsQ<R, Q> lds;
     const int part_r = P.part_off + b;
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
@@ -1426,7 +1451,7 @@ void k_iter_persist(IterParams<R, VT> P, int n_iter)
             __shared__ WnLds<R> lds_wn;
             wn_tile<R, VT, ENG, true>(P, tile, it, parity, T, part_r, lds_wn, j == 0);
         } else {
-            __shared__ TileLds<R, BLOCK / Q> lds;
+            __shared__ TileLdsQ<R, Q> lds;
             if (edge_first)
                 iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, parity, part_r, lds, 0, P.L, T, j > 0);
             else
@@ -1659,7 +1684,8 @@ struct gqmap_ctx {
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
-    int split = 1;      // lanes per node (Q): 1, 4 or 16
+    int split = 1;      // lanes per node of the arithmetic (Q): 1, 2, 4, 8, 16, 64
+    int kq = 1;         // kernel shape: split, or 0 = role split (Q = 1 arithmetic, 16 x 8 tiles)
     int lpar = 1;       // k_iter blocks per tile (components spread over blocks)
     hipGraphExec_t graph = nullptr;
     bool own_stream = true;
@@ -1737,7 +1763,12 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     // from the whole grid (Ng columns), so every column-strip tile sums its
     // quadrature in the same order as the untiled solve
     c->split = choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
-    const int tr = tile_rows(c->split), tc = tile_cols(c->split);
+    c->kq = c->split;
+    if (c->opt.split == GQMAP_SPLIT_ROLE && !c->super_) {  // role split: Q = 1 arithmetic
+        c->split = 1;
+        c->kq = 0;
+    }
+    const int tr = tile_rows(c->kq), tc = tile_cols(c->kq);
     c->tiles_m = (c->M + tr - 1) / tr;
     c->tiles_n = (c->N + tc - 1) / tc;
     c->lpar = choose_lpar(c);
@@ -1851,7 +1882,7 @@ struct TileSegs {
 // [0, bnd) and [bnd, nblocks).
 void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
 {
-    const int TN = tile_cols(c->split);  // tile columns
+    const int TN = tile_cols(c->kq);  // tile columns
     const int tm = c->tiles_m, cb0 = c->own_lo / TN, cb1 = (c->own_hi - 1) / TN;
     bnd.lo[0] = cb0 * tm; bnd.n[0] = tm;
     bnd.lo[1] = cb1 * tm; bnd.n[1] = cb1 != cb0 ? tm : 0;
@@ -1916,7 +1947,8 @@ template <typename R, typename VT, int ENG>
 void launch_iter_q(gqmap_ctx *c, const TileSegs *sg)
 {
     if constexpr (ENG != 1) {
-        if (c->split == 64) return launch_k_iter_wn<R, VT, ENG>(c, sg);
+        if (c->kq == 64) return launch_k_iter_wn<R, VT, ENG>(c, sg);
+        if (c->kq == 0) return launch_k_iter<R, VT, ENG, 0>(c, sg);
     }
     if (c->split == 16)
         launch_k_iter<R, VT, ENG, 16>(c, sg);
@@ -1999,7 +2031,7 @@ template <typename R, typename VT>
 bool launch_persist_t(gqmap_ctx *c, int n, bool dry)
 {
     // not Q = 4 (120x160): 57.3 vs 48.8 us/it measured (profiles/r03_persist_levels.txt)
-    switch (c->split) {
+    switch (c->kq) {
     case 8: return launch_persist_q<R, VT, 8>(c, n, dry);
     case 16: return launch_persist_q<R, VT, 16>(c, n, dry);
     case 64: return launch_persist_q<R, VT, 64>(c, n, dry);
@@ -2426,6 +2458,13 @@ void ctx_adopt_stream(gqmap_ctx *c, hipStream_t s)
 extern "C" {
 
 int gqmap_abi_version(void) { return GQMAP_ABI_VERSION; }
+
+// Not in include/gqmap.h (tests): the k_iter kernel shape a context runs --
+// lanes per node, 0 for the role split (GQMAP_SPLIT_ROLE); -1 without a grid.
+int gqmap_debug_kernel_shape(const gqmap_ctx *c)
+{
+    return c && c->have_images ? c->kq : -1;
+}
 
 #if GQ_TIMELINE
 // debug builds only (not in include/gqmap.h): copy the k_iter timeline

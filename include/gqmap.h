@@ -53,6 +53,8 @@ typedef enum gqmap_engine_kind {
 } gqmap_engine_kind;
 
 typedef enum gqmap_precision { GQMAP_FP64 = 0, GQMAP_FP32 = 1 } gqmap_precision;
+/* gqmap_options.split: Q = 1 arithmetic, node and edge phases on separate waves */
+#define GQMAP_SPLIT_ROLE (-1)
 typedef enum gqmap_alpha_mode {
     GQMAP_ALPHA_SOFTMAX = 0,   /* updateAlpha, gqmap_gpu_mixture.m:78-86 (live path)   */
     GQMAP_ALPHA_PROJSPLX = 1   /* projsplx(alpha+dalpha*step*lr), :49 (commented out)   */
@@ -80,8 +82,10 @@ typedef struct gqmap_options {
     double sig_lo, sig_hi;  /* 0.01 / 23 mixture (:43-44), 0.01 / 25 super       */
     double corr_tor;     /* 1-1e-5 (:7)                                          */
     double tor;          /* 1e-4 stop threshold on ptdmu (:25,75)                */
-    int split;           /* lanes per node Q (1/2/4/16), 0 = auto from the grid size;
-                            part of the arithmetic (partial quadrature sums)    */
+    int split;           /* lanes per node Q (1/2/4/8/16/64), 0 = auto from the grid
+                            size; part of the arithmetic (partial quadrature sums);
+                            GQMAP_SPLIT_ROLE: Q = 1 arithmetic with the node and
+                            edge phases on separate waves (mid-size grids)       */
     double sig_step;     /* sigma step scale: 1, ctf 0.3 (gqmap_ctf.m:34-35)     */
     double sig_init;     /* init sigma = U + sig_init; < 0: U + (max - min)      */
 } gqmap_options;

@@ -253,7 +253,9 @@ def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
     cs = state.cstruct()
     f = lib().emu_run
     f.restype = C.c_int
-    Q = int(opts.get("split", 0)) or (split_for(p.M, p.N, bool(p.super_), int(p.L)) if split is None else split)
+    Q = int(opts.get("split", 0))
+    Q = 1 if Q == -1 else Q  # GQMAP_SPLIT_ROLE: a kernel shape with the Q = 1 arithmetic
+    Q = Q or (split_for(p.M, p.N, bool(p.super_), int(p.L)) if split is None else split)
     done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
              _p(trace), nthreads, int(fp32), Q)
     if done < 0:

@@ -2,7 +2,7 @@
 path (prepared graph, 100 iterations after 10), for A/B of libgqmap builds
 (GQMAP_LIB) and GQMAP_NO_PERSIST.  Timing only: the variants built with the
 GQ_PERSIST_* experiment switches do not produce valid results.
-usage: persist_ab.py [fp64|fp32] [scales]"""
+usage: [SPLIT=q] persist_ab.py [fp64|fp32] [scales]  (SPLIT=-1: role split)"""
 import os
 import sys
 import time
@@ -15,11 +15,13 @@ from gqmap_opticalflow_amd import Engine, ctf_options, imresize  # noqa: E402
 
 prec = sys.argv[1] if len(sys.argv) > 1 else "fp64"
 scales = [float(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0.0625, 0.125, 0.25]
-lab = os.path.basename(os.environ.get("GQMAP_LIB", "libgqmap.so")) + (" no-persist" if os.environ.get("GQMAP_NO_PERSIST") else "")
+lab = os.path.basename(os.environ.get("GQMAP_LIB", "libgqmap.so")) + (" no-persist" if os.environ.get("GQMAP_NO_PERSIST") else "") \
+    + (" split=" + os.environ["SPLIT"] if os.environ.get("SPLIT") else "")
 I1, I2, flo, unk, o = gt_options("Grove3", 1, 11)
 for s in scales:
     a, b = (np.asfortranarray(imresize(x, s)) for x in (I1, I2))
-    opts = ctf_options(its=500, minu=o["minu"], maxu=o["maxu"], minv=o["minv"], maxv=o["maxv"])
+    opts = ctf_options(its=500, minu=o["minu"], maxu=o["maxu"], minv=o["minv"], maxv=o["maxv"],
+                       split=int(os.environ.get("SPLIT", "0")))
     with Engine(opts, a, b, "ctf", prec) as e:
         best = 1e9
         for rep in range(3):
