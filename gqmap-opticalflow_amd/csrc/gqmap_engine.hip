@@ -149,6 +149,11 @@ struct Ctl {
     // them.  One slice per XCD (blocks go round-robin to the 8 XCDs): fewer
     // atomics on one address when a small grid's workgroups end together.
     unsigned long long acc[ACC_SLICES][NFIX + GQMAP_LMAX][4];
+    // speculative RCCL tiles (L = 1): the iteration the kernels run next --
+    // advanced by the ghost unpack, ahead of it / done / T, which the
+    // finalize advances when it has judged the stop rule (launch_step_rccl_spec)
+    int it_i, done_i;
+    double T_i;
 };
 
 struct FinParams {
@@ -214,6 +219,7 @@ struct IterParams {
     int guard;
     int64_t MNL;
     unsigned *bar;  // k_iter_persist: barrier counters (BAR_WORDS, zero between launches)
+    int spec;       // speculative RCCL tile: run iteration Ctl::it_i / done_i / T_i
 };
 
 // Quadrature tables are read with wave-uniform indices; routing them through
@@ -1068,9 +1074,11 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
     } else if (edge_first)
-        iter_tile<R, VT, ENG, Q, true>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1, ctl->T, false);
+        iter_tile<R, VT, ENG, Q, true>(P, tile, P.spec ? ctl->it_i : ctl->it, (P.spec ? ctl->done_i : ctl->done) & 1,
+                                       part_r, lds, l0, l1, P.spec ? ctl->T_i : ctl->T, false);
     else
-        iter_tile<R, VT, ENG, Q, false>(P, tile, ctl->it, ctl->done & 1, part_r, lds, l0, l1, ctl->T, false);
+        iter_tile<R, VT, ENG, Q, false>(P, tile, P.spec ? ctl->it_i : ctl->it, (P.spec ? ctl->done_i : ctl->done) & 1,
+                                        part_r, lds, l0, l1, P.spec ? ctl->T_i : ctl->T, false);
 #if GQ_TIMELINE
     __syncthreads();
     TL_STAMP(0, tl0);
@@ -1282,7 +1290,8 @@ __global__ __launch_bounds__(WN_THREADS, 1) void k_iter_wn(IterParams<R, VT> P)
     const int tl = tile_of_block(b, nb, 1, P.cu_slots);
     const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
     __shared__ WnLds<R> lds;
-    wn_tile<R, VT, ENG, false>(P, tile, ctl->it, ctl->done & 1, ctl->T, P.part_off + b, lds, true);
+    wn_tile<R, VT, ENG, false>(P, tile, P.spec ? ctl->it_i : ctl->it, (P.spec ? ctl->done_i : ctl->done) & 1,
+                               P.spec ? ctl->T_i : ctl->T, P.part_off + b, lds, true);
     TL_STAMP(0, tl0);
     TL_STAMP(4, __builtin_amdgcn_s_memrealtime());
     if (P.fused) fused_finalize_tail(P.fin);
@@ -1525,10 +1534,10 @@ struct HaloSide {
 // the strip ends have one).
 template <typename R>
 __global__ void k_halo_copy(const Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL, int L,
-                            HaloSide<R> s0, HaloSide<R> s1)
+                            HaloSide<R> s0, HaloSide<R> s1, int spec)
 {
     if (ctl->stop) return;
-    R *dst = (ctl->done & 1) ? st0 : st1;
+    R *dst = ((spec ? ctl->done_i : ctl->done) & 1) ? st0 : st1;
     const HaloSide<R> &hs = blockIdx.y == 0 ? s0 : s1;
     const int col = hs.col, np = hs.np;
     const uint32_t planes = hs.planes;
@@ -1568,7 +1577,44 @@ __global__ __launch_bounds__(256) void k_unpack_finalize(FinParams F, R *st0, R 
     __shared__ fix128 sh[256];
     __shared__ double tot[NFIX + GQMAP_LMAX];
     fin_reduce(F, tot, sh);  // (its barriers order every thread's parity read before fin_apply)
-    if (threadIdx.x == 0) fin_apply(F, tot);
+    if (threadIdx.x == 0) {
+        fin_apply(F, tot);
+        ctl->it_i = ctl->it;  // the speculative counters follow (a later spec run starts here)
+        ctl->done_i = ctl->done;
+        ctl->T_i = ctl->T;
+    }
+}
+
+// Speculative RCCL tile (L = 1): the received ghost columns into the state
+// buffer the iteration just wrote, then the iteration counters the kernels
+// run by -- the same steps fin_apply takes (temperature decay after
+// iteration it_i, it + 1, done + 1), without waiting for the totals: nothing
+// of the next iteration depends on them but the stop rule, which the
+// finalize (k_finalize, on its own stream) judges one iteration behind.
+template <typename R>
+__global__ __launch_bounds__(256) void k_unpack_advance(Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL,
+                                                        int L, HaloSide<R> s0, HaloSide<R> s1, int nsides,
+                                                        int t_decay_every, double drate, double t_min)
+{
+    if (ctl->stop) return;
+    R *dst = (ctl->done_i & 1) ? st0 : st1;
+    for (int k = 0; k < nsides; ++k) {
+        const HaloSide<R> &hs = k == 0 ? s0 : s1;
+        const int64_t n = (int64_t)hs.np * L * M;
+        for (int64_t t = threadIdx.x; t < n; t += 256) {
+            const int m = (int)(t % M);
+            const int64_t ql = t / M;
+            const int q = (int)((hs.planes >> (4 * (int)(ql / L))) & 15u), l = (int)(ql % L);
+            dst[(int64_t)q * MNL + (int64_t)l * MN + (int64_t)hs.col * M + m] = hs.buf[t];
+        }
+    }
+    __syncthreads();  // every thread's parity read before the advance
+    if (threadIdx.x == 0) {
+        const int it = ctl->it_i;
+        if (t_decay_every > 0 && it % t_decay_every == 0) ctl->T_i = fmax(ctl->T_i * drate, t_min);
+        ctl->it_i = it + 1;
+        ctl->done_i = ctl->done_i + 1;
+    }
 }
 
 template <typename R>
@@ -1709,6 +1755,17 @@ struct gqmap_ctx {
     // tiles run on `stream` (fork / join events)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_bnd = nullptr, ev_inr = nullptr, ev_xch = nullptr;
+    // speculative RCCL step (L = 1, launch_step_rccl_spec): boundary tiles on
+    // `bnd`, the exchange and the totals' all-gather on `side`, the finalize on
+    // `fin`; the totals table is double-buffered by the iteration's parity
+    // within a joined sequence (`issued`), and iteration j waits only for the
+    // finalize of iteration j - 2 (ev_fin[j & 1])
+    hipStream_t bnd = nullptr, fin = nullptr;
+    hipEvent_t ev_ag = nullptr, ev_fin[2] = {nullptr, nullptr};
+    bool fin_pending[2] = {false, false};
+    int issued = 0;
+    bool spec_now = false;      // the launches being issued belong to a speculative step
+    fix128 *gbuf = nullptr;     // this step's half of d_gathered
 };
 
 namespace {
@@ -1831,7 +1888,9 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     // k_reduce_local between the launches and the all-gather)
     P.tile_acc = c->comm != nullptr;
     P.ticket_total = c->nblocks;
-    P.tile_totals = c->d_gathered ? c->d_gathered + (size_t)c->tile * (NFIX + c->L) : nullptr;
+    fix128 *gt = c->gbuf ? c->gbuf : c->d_gathered;
+    P.tile_totals = gt ? gt + (size_t)c->tile * (NFIX + c->L) : nullptr;
+    P.spec = c->spec_now ? 1 : 0;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     P.bar = c->d_bar;
@@ -1849,7 +1908,7 @@ FinParams fin_params(const gqmap_ctx *c)
     F.trace = c->d_trace;
     F.aepe = c->d_truth != nullptr;
     F.count = (double)(c->M - 2) * (double)(c->Ng - 2) * c->L;  // global interior
-    F.gathered = c->d_gathered;
+    F.gathered = c->gbuf ? c->gbuf : c->d_gathered;
     F.nranks = c->nranks;
     F.step0 = o.step0; F.step_decay = o.step_decay;
     F.alpha_mode = o.alpha_mode; F.alpha_start = o.alpha_start; F.alpha_lr = o.alpha_lr;
@@ -2121,7 +2180,7 @@ void halo_copy(gqmap_ctx *c, hipStream_t s, const HaloSide<R> *sides, int nsides
     const int grid = (int)std::min<int64_t>((n + 255) / 256, 1024);
     k_halo_copy<R><<<dim3(grid, nsides), 256, 0, s>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M,
                                                      (int64_t)c->M * c->N, c->MNL, c->L, sides[0],
-                                                     sides[nsides - 1]);
+                                                     sides[nsides - 1], c->spec_now ? 1 : 0);
 }
 
 // This tile's boundary columns -> d_halo[0] (to the left neighbour, tile - 1)
@@ -2225,9 +2284,116 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     return GQMAP_OK;
 }
 
+// Speculative RCCL step for L = 1 (rccl_spec below).  Nothing of iteration j + 1 depends on iteration j's totals
+// but the stop rule, so the all-gather of the totals and the finalize leave
+// the critical path: per iteration
+//   main  [wait finalize(j-2)] fork | interior k_iter | wait exchange | unpack + advance (k_unpack_advance)
+//   bnd   boundary k_iter, pack
+//   side  send/recv (after pack) | all-gather of the totals (after both k_iter launches)
+//   fin   k_finalize (after the all-gather): trace, T / it / done, stop rule
+// Iteration j + 1 may run before finalize(j) has judged iteration j: if j met
+// the rule, j + 1 wrote only the buffer that held state j - 1 (Ctl::done still
+// points at state j) and finalize(j + 1) returns on the stop flag; iteration
+// j + 2 waits for finalize(j) and turns into no-ops.  RCCL calls stay on one
+// stream in one order on every rank.  Totals of iteration j live in half
+// (j & 1) of d_gathered: half j & 1 is rewritten by iteration j + 2, which
+// starts after finalize(j).
+// Default: on when there are other ranks (a real collective to hide); behind
+// a one-rank communicator it measured no gain (profiles/r03_strip_spec.txt).
+// GQMAP_SPEC=1 / 0 forces it on / off (tests run it on one rank).
+bool rccl_spec(const gqmap_ctx *c)
+{
+    if (!c->comm || c->L != 1) return false;
+    const char *e = std::getenv("GQMAP_SPEC");
+    if (e && *e) return *e == '1';
+    return c->n_tiles > 1;
+}
+
+template <typename R>
+void unpack_advance_t(gqmap_ctx *c)
+{
+    HaloSide<R> sd[2];
+    int n = 0;
+    if (c->tile > 0) sd[n++] = HaloSide<R>{0, HALO_TO_RIGHT_N, HALO_TO_RIGHT, (R *)c->d_halo[2]};
+    if (c->tile < c->n_tiles - 1) sd[n++] = HaloSide<R>{c->N - 1, HALO_TO_LEFT_N, HALO_TO_LEFT, (R *)c->d_halo[3]};
+    if (n == 0) sd[0] = HaloSide<R>{0, 0, 0u, nullptr};
+    k_unpack_advance<R><<<1, 256, 0, c->stream>>>(c->d_ctl, (R *)c->d_st[0], (R *)c->d_st[1], c->M,
+                                                  (int64_t)c->M * c->N, c->MNL, c->L, sd[0], sd[n > 0 ? n - 1 : 0], n,
+                                                  c->opt.t_decay_every, c->opt.drate, c->opt.t_min);
+}
+
+gqmap_status launch_step_rccl_spec(gqmap_ctx *c)
+{
+    const int NP = NFIX + c->L, r = c->comm->rank;
+    const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
+    const size_t nl = (size_t)HALO_TO_LEFT_N * c->L * c->M, nr = (size_t)HALO_TO_RIGHT_N * c->L * c->M;
+    const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
+    const Rccl *R = rccl();
+    TileSegs bnd, inr;
+    tile_segments(c, bnd, inr);
+    const int par = c->issued & 1;
+    c->issued++;
+    c->gbuf = c->d_gathered + (size_t)par * c->n_tiles * NP;
+    c->spec_now = true;
+    hipStream_t main_stream = c->stream;
+    // the stop verdict on iteration j - 2 before iteration j starts
+    if (c->fin_pending[par]) GQ_HIP(hipStreamWaitEvent(main_stream, c->ev_fin[par], 0));
+    GQ_HIP(hipEventRecord(c->ev_fork, main_stream));
+    GQ_HIP(hipStreamWaitEvent(c->bnd, c->ev_fork, 0));
+    c->stream = c->bnd;
+    launch_iter(c, &bnd);
+    halo_pack(c, c->bnd);
+    c->stream = main_stream;
+    GQ_HIP(hipEventRecord(c->ev_bnd, c->bnd));
+    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_bnd, 0));
+    GQ_NCCL(R->GroupStart());
+    if (left) {
+        GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->side));
+        GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->side));
+    }
+    if (right) {
+        GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->side));
+        GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->side));
+    }
+    GQ_NCCL(R->GroupEnd());
+    GQ_HIP(hipEventRecord(c->ev_xch, c->side));
+    launch_iter(c, &inr);
+    GQ_HIP(hipEventRecord(c->ev_inr, main_stream));
+    // the totals (written by the last workgroup of the two launches)
+    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_inr, 0));
+    GQ_NCCL(R->AllGather(c->gbuf + (size_t)r * NP, c->gbuf, (size_t)NP * sizeof(fix128), ncclUint8, c->comm->comm,
+                         c->side));
+    GQ_HIP(hipEventRecord(c->ev_ag, c->side));
+    GQ_HIP(hipStreamWaitEvent(c->fin, c->ev_ag, 0));
+    k_finalize<<<1, 256, 0, c->fin>>>(fin_params(c));
+    GQ_HIP(hipEventRecord(c->ev_fin[par], c->fin));
+    c->fin_pending[par] = true;
+    GQ_HIP(hipStreamWaitEvent(main_stream, c->ev_xch, 0));
+    if (c->fp32) unpack_advance_t<float>(c);
+    else unpack_advance_t<double>(c);
+    c->spec_now = false;
+    c->gbuf = nullptr;
+    return GQMAP_OK;
+}
+
+// The end of a speculative sequence: every finalize joined into the context
+// stream (also what a stream capture needs to close), parity restarts.
+gqmap_status join_spec(gqmap_ctx *c)
+{
+    for (int p = 0; p < 2; ++p)
+        if (c->fin_pending[p]) {
+            GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_fin[p], 0));
+            c->fin_pending[p] = false;
+        }
+    c->issued = 0;
+    c->spec_now = false;
+    c->gbuf = nullptr;
+    return GQMAP_OK;
+}
+
 gqmap_status launch_step(gqmap_ctx *c)
 {
-    if (c->comm) return launch_step_rccl(c);
+    if (c->comm) return rccl_spec(c) ? launch_step_rccl_spec(c) : launch_step_rccl(c);
     launch_iter(c);
     return launch_tail(c);
 }
@@ -2238,6 +2404,7 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
     if (launch_persist(c, n)) return GQMAP_OK;
     gqmap_status st = GQMAP_OK;
     for (int i = 0; i < n && st == GQMAP_OK; ++i) st = launch_step(c);
+    if (st == GQMAP_OK && rccl_spec(c)) st = join_spec(c);
     return st;
 }
 
@@ -2266,6 +2433,9 @@ gqmap_status upload_ctl(gqmap_ctx *c, int it, double T, const double *w, const d
     h.done = 0;
     h.stop = 0;
     h.T = T;
+    h.it_i = it;
+    h.done_i = 0;
+    h.T_i = T;
     for (int l = 0; l < c->L; ++l) {
         h.w[l] = w[l];
         h.alpha[l] = alpha[l];
@@ -3099,8 +3269,9 @@ gqmap_status gqmap_create_tile(gqmap_ctx **out, const gqmap_options *opt, int de
 static gqmap_status attach_common(gqmap_ctx *c)
 {
     const size_t NP = NFIX + c->L;
-    GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles));
-    GQ_HIP(hipMemsetAsync(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles, c->stream));
+    // two halves: the speculative RCCL step alternates them by iteration parity
+    GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles * 2));
+    GQ_HIP(hipMemsetAsync(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles * 2, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     c->own_gathered = true;
     c->nranks = c->n_tiles;
@@ -3145,7 +3316,9 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
     gqmap_status s = attach_common(c);
     if (s != GQMAP_OK) return s;
     GQ_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    for (hipEvent_t *e : {&c->ev_fork, &c->ev_bnd, &c->ev_inr, &c->ev_xch})
+    GQ_HIP(hipStreamCreateWithFlags(&c->bnd, hipStreamNonBlocking));
+    GQ_HIP(hipStreamCreateWithFlags(&c->fin, hipStreamNonBlocking));
+    for (hipEvent_t *e : {&c->ev_fork, &c->ev_bnd, &c->ev_inr, &c->ev_xch, &c->ev_ag, &c->ev_fin[0], &c->ev_fin[1]})
         GQ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     return GQMAP_OK;
 }
@@ -3324,10 +3497,12 @@ void gqmap_destroy(gqmap_ctx *c)
         (void)rccl()->CommDestroy(c->comm->comm);
         delete c->comm;
     }
-    if (c->side) (void)hipStreamSynchronize(c->side);
-    for (hipEvent_t e : {c->ev_fork, c->ev_bnd, c->ev_inr, c->ev_xch})
+    for (hipStream_t st : {c->side, c->bnd, c->fin})
+        if (st) (void)hipStreamSynchronize(st);
+    for (hipEvent_t e : {c->ev_fork, c->ev_bnd, c->ev_inr, c->ev_xch, c->ev_ag, c->ev_fin[0], c->ev_fin[1]})
         if (e) (void)hipEventDestroy(e);
-    if (c->side) (void)hipStreamDestroy(c->side);
+    for (hipStream_t st : {c->side, c->bnd, c->fin})
+        if (st) (void)hipStreamDestroy(st);
     if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);

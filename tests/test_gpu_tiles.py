@@ -242,3 +242,62 @@ def test_c2_pair_strips_at_per_strip_split_bit_exact(n_tiles):
     finally:
         for t in tiles:
             t.close()
+
+
+def test_single_rank_rccl_speculative_step_l1(monkeypatch):
+    """L = 1 RCCL tiles take the speculative step (launch_step_rccl_spec: the
+    totals' all-gather and the finalize off the critical path, the stop rule
+    judged one iteration behind; forced on for one rank, the default with
+    more): bit-identical to the whole grid over replayed graphs + leftover
+    launches with the temperature decay on, and a run_timed (the
+    non-speculative step) in between keeps the counters."""
+    from gqmap_opticalflow_amd import Engine, comm_unique_id
+    monkeypatch.setenv("GQMAP_SPEC", "1")
+    I1, I2, o = _problem("mixture", 1)
+    o = dict(o, temperature=0.3, t_decay_every=7)
+    init, ref, tr = _whole(I1, I2, o, "mixture", "fp64", 133, seed=1)
+    e = Engine(o, I1, I2, n_tiles=1, tile=0)
+    try:
+        e.attach_rccl(comm_unique_id())
+        e.set_state(init.copy())
+        done, t1 = e.run(61)   # one graph + 11 launches
+        done2, _, _ = e.run_timed(11)
+        done3, t3 = e.run(61)
+        assert (done, done2, done3) == (61, 11, 61)
+        np.testing.assert_array_equal(t1, tr[:61])
+        np.testing.assert_array_equal(t3, tr[72:133])
+        got = e.get_state()
+        for k in G.STATE_KEYS:
+            np.testing.assert_array_equal(getattr(got, k), getattr(ref, k), err_msg=k)
+        assert got.T == ref.T and got.it == ref.it
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("k", [0, 23, 49, 57])
+def test_single_rank_rccl_speculative_stop(k, monkeypatch):
+    # the stop rule met at row k (inside a graph chunk, at its last iteration,
+    # in the leftover launches): the speculative iteration after it leaves no
+    # trace; the state is the whole grid's after k + 1 iterations
+    from gqmap_opticalflow_amd import Engine, comm_unique_id
+    monkeypatch.setenv("GQMAP_SPEC", "1")
+    I1, I2, o = _problem("mixture", 1)
+    init, _, tr = _whole(I1, I2, o, "mixture", "fp64", 70, seed=1)
+    ptd = tr[:, 1]
+    tor = 1e9 if k == 0 else float(ptd[k]) * (1 + 1e-12)
+    k = int(np.argmax(ptd < tor))
+    o = dict(o, tor=tor)
+    _, ref, tr_ref = _whole(I1, I2, o, "mixture", "fp64", 70, seed=1)
+    e = Engine(o, I1, I2, n_tiles=1, tile=0)
+    try:
+        e.attach_rccl(comm_unique_id())
+        e.set_state(init.copy())
+        done, t2 = e.run(70)
+        assert done == k + 1 and e.info().stopped == 1
+        np.testing.assert_array_equal(t2, tr_ref)
+        got = e.get_state()
+        for key in G.STATE_KEYS:
+            np.testing.assert_array_equal(getattr(got, key), getattr(ref, key), err_msg=key)
+        assert e.run(20)[0] == 0
+    finally:
+        e.close()
