@@ -18,6 +18,7 @@ GQMAP_OK = 0
 ENGINE_MIXTURE, ENGINE_SUPER, ENGINE_CTF = 0, 1, 2
 FP64, FP32 = 0, 1
 ALPHA_SOFTMAX, ALPHA_PROJSPLX = 0, 1
+SPLIT_ROLE = -1  # GQMAP_SPLIT_ROLE: options["split"] for the role-split kernel shape (Q = 1 arithmetic)
 LMAX, KMAX = 8, 16
 
 # Every entry point declared in include/gqmap.h (checked by tests/test_abi.py).

@@ -31,6 +31,17 @@ def test_library_exports_every_declared_symbol():
     assert lib.gqmap_abi_version() == 1
 
 
+def test_header_constants_mirrored():
+    # enum values and #defines of include/gqmap.h that the Python mirror restates
+    from gqmap_opticalflow_amd import _lib
+    src = open(HEADER).read()
+    consts = {k: int(v) for k, v in re.findall(r"\b(GQMAP_[A-Z0-9_]+)\s*=\s*(-?\d+)", src)}
+    consts.update({k: int(v) for k, v in re.findall(r"#define\s+(GQMAP_[A-Z0-9_]+)\s+\(?(-?\d+)\)?", src)})
+    assert consts["GQMAP_ENGINE_CTF"] == _lib.ENGINE_CTF and consts["GQMAP_FP32"] == _lib.FP32
+    assert consts["GQMAP_ALPHA_PROJSPLX"] == _lib.ALPHA_PROJSPLX
+    assert consts["GQMAP_SPLIT_ROLE"] == _lib.SPLIT_ROLE
+
+
 def test_library_is_built_for_gfx950():
     from gqmap_opticalflow_amd import _lib
     blob = open(_lib.LIB_PATH, "rb").read()

@@ -15,7 +15,7 @@ from tests.test_gpu_tiles import _assemble, _problem
 
 pytestmark = pytest.mark.gpu
 
-ROLE = -1  # GQMAP_SPLIT_ROLE
+ROLE = -1  # GQMAP_SPLIT_ROLE (gqmap_opticalflow_amd._lib.SPLIT_ROLE)
 
 
 def _shape(eng):
