@@ -647,6 +647,9 @@ __device__ __forceinline__ bool node_interior(const IterParams<R, VT> &P, int mm
 #ifndef GQ_PERSIST_NOFIN  // timing experiment only (no trace / stop): the finalizer only arrives
 #define GQ_PERSIST_NOFIN 0
 #endif
+#ifndef GQ_PERSIST_Q4
+#define GQ_PERSIST_Q4 0
+#endif
 #ifndef GQ_PERSIST_SLEEP
 #define GQ_PERSIST_SLEEP 2
 #endif
@@ -2080,7 +2083,8 @@ bool launch_persist_q(gqmap_ctx *c, int n, bool dry)
     P.fin.nblocks = 2 * G;  // partial row stride: iteration j writes rows (j & 1) * G + b
     const int threads = Q == 64 ? WN_THREADS : BLOCK;
     static const int2 shape = kernel_shape(k_iter_persist<R, VT, 2, Q>);
-    P.cu_group = Q == 64 ? 1 : shape.x;
+    static const bool no_group = std::getenv("GQMAP_NO_CU_GROUP") != nullptr;
+    P.cu_group = Q == 64 || no_group ? 1 : shape.x;
     P.cu_slots = std::max(1, shape.y / 8);
     k_iter_persist<R, VT, 2, Q><<<G + 1, threads, 0, c->stream>>>(P, n);
     return true;
@@ -2089,7 +2093,11 @@ bool launch_persist_q(gqmap_ctx *c, int n, bool dry)
 template <typename R, typename VT>
 bool launch_persist_t(gqmap_ctx *c, int n, bool dry)
 {
-    // not Q = 4 (120x160): 57.3 vs 48.8 us/it measured (profiles/r03_persist_levels.txt)
+    // not Q = 4 (120x160): 57.3 vs 48.8 us/it measured (profiles/r03_persist_levels.txt;
+    // GQ_PERSIST_Q4: experiment builds only)
+#if GQ_PERSIST_Q4
+    if (c->kq == 4) return launch_persist_q<R, VT, 4>(c, n, dry);
+#endif
     switch (c->kq) {
     case 8: return launch_persist_q<R, VT, 8>(c, n, dry);
     case 16: return launch_persist_q<R, VT, 16>(c, n, dry);
