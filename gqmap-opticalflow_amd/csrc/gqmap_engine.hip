@@ -151,8 +151,11 @@ struct Ctl {
     unsigned long long acc[ACC_SLICES][NFIX + GQMAP_LMAX][4];
     // speculative RCCL tiles (L = 1): the iteration the kernels run next --
     // advanced by the ghost unpack, ahead of it / done / T, which the
-    // finalize advances when it has judged the stop rule (launch_step_rccl_spec)
-    int it_i, done_i;
+    // finalize advances when it has judged the stop rule (launch_step_rccl_spec).
+    // A cache line of their own: the two kernels that write them and it / done
+    // / T may run at the same time on different XCDs.
+    alignas(128) int it_i;
+    int done_i;
     double T_i;
 };
 
