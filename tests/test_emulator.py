@@ -70,3 +70,18 @@ def test_deterministic_math_within_one_ulp(oracle_lib):
     assert oracle_lib.emu_math(2, [-800.0])[0] == 0.0
     s = rng.uniform(1e-6, 1e4, 1000)
     np.testing.assert_array_equal(oracle_lib.emu_math(0, s), np.sqrt(s))
+
+
+def test_emulator_role_split_option_is_the_q1_arithmetic(oracle_lib):
+    # options["split"] = GQMAP_SPLIT_ROLE (-1) names a kernel shape with the
+    # Q = 1 arithmetic: the CPU model run with it equals split 1 bit for bit
+    d = G.load("mixture_L3_T")
+    X, W = _gh(9)
+    res = []
+    for split in (1, -1):
+        st = oracle_lib.State(*G.state(d).values())
+        _, tr, _ = oracle_lib.emu_run(dict(d["opts"], split=split), d["I1"], d["I2"], st, 1, 3, X, W)
+        res.append((tr, st.arrays()))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        np.testing.assert_array_equal(a, b)
