@@ -16,7 +16,10 @@
 //
 // All loop control lives on the device (Ctl), so a chunk of iterations is
 // captured once into a hipGraph and replayed; a stopped run turns the
-// remaining launches into no-ops.
+// remaining launches into no-ops.  (Normally the finalize is fused into the
+// last k_iter workgroup.  The smallest coarse-to-fine levels run a whole
+// chunk in one k_iter_persist launch; column-strip tiles over RCCL add the
+// ghost-column exchange and, for L = 1, finalize one iteration behind.)
 //
 // Layout: every field is a MATLAB column-major plane (m fastest).  A state
 // buffer is 9 planes of M*N*L: muu, muv, sigu, sigv, pn, rou(dir=1,u),
