@@ -127,43 +127,127 @@ def _timed_leg(run_n, budget_s):
     return done, time.perf_counter() - t0
 
 
-def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 8.0, allcores: bool = False):
-    """The oracle (literal C fp64 restatement of the engine loop, OpenMP over
-    rows) on this host's cores -- every core this process may use, then one
-    thread -- on a bounded sample of the same workload."""
-    from gqmap_opticalflow_amd import initial_state
+def allcore_threads(hc) -> int:
+    """Every physical core this process may run on (BASELINE.md:51: "all host
+    cores of the GPU box")."""
+    return max(1, min(hc["physical_cores"] or hc["affinity"], hc["affinity"]))
+
+
+def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 6.0, split: int | None = None,
+                 precision: str = "fp64"):
+    """The CPU paths on this host's cores, each on a bounded sample of the
+    same workload from the same seeded init:
+      * the literal C fp64 restatement of the engine loop (oracle/gqmap_oracle.c,
+        OpenMP over rows) on this process's CPU share (`value`), on one
+        thread, and on every physical core (`value_allcores`);
+      * the CPU model of the kernel arithmetic (oracle/gqmap_emul.cpp) -- the
+        CPU path the GPU matches bit for bit -- on the same share
+        (`value_emul`) and on every physical core."""
+    from gqmap_opticalflow_amd import gauss_hermite, initial_state
     from oracle import oracle
     hc = host_cpus()
     Mo, No = I1.shape
     M, N = (Mo // 4, No // 4) if engine == "super" else (Mo, No)
     o = dict(opts, engine=engine)
-    legs = {}
-    counts = [hc["threads"], 1]
-    if allcores and hc["physical_cores"] and hc["physical_cores"] != hc["threads"]:
-        counts.append(min(hc["physical_cores"], hc["affinity"]))
-    for threads in counts:
+    X, W = gauss_hermite(int(opts["K"]))
+    allc = allcore_threads(hc)
+
+    def leg(kind, threads):
         st0 = initial_state(o, M, N, seed=0, engine=engine)
         st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
-        it = [1]
+        it, T = [1], [st0.T]
 
-        def run_n(n, st=st, threads=threads):
-            done, _, _ = oracle.run(o, I1, I2, st, it[0], n, nthreads=threads)
+        def run_n(n):
+            if kind == "literal":
+                done, _, T[0] = oracle.run(o, I1, I2, st, it[0], n, T=T[0], nthreads=threads)
+            else:
+                done, _, T[0] = oracle.emu_run(o, I1, I2, st, it[0], n, X, W, T=T[0], nthreads=threads,
+                                               fp32=precision == "fp32", split=split)
             it[0] += done
             return done
-        legs[threads] = _timed_leg(run_n, budget_s)
-    (n_all, t_all), (n_one, t_one) = legs[hc["threads"]], legs[1]
-    extra = {}
-    if len(counts) > 2:
-        n_pc, t_pc = legs[counts[2]]
-        extra = {"value_allcores": Mo * No * n_pc / t_pc / 1e9, "cores_allcores": counts[2]}
-    return {"value": Mo * No * n_all / t_all / 1e9, "unit": "Gpixel-iter/s", "cores": hc["threads"],
-            "kind": "port", "value_1thread": Mo * No * n_one / t_one / 1e9, **extra,
+        n, t = _timed_leg(run_n, budget_s)
+        return Mo * No * n / t / 1e9, n, t
+
+    v_sh, n_sh, t_sh = leg("literal", hc["threads"])
+    v_1, n_1, t_1 = leg("literal", 1)
+    v_all, n_all, t_all = leg("literal", allc)
+    v_em, n_em, t_em = leg("emul", hc["threads"])
+    v_ema, n_ema, t_ema = leg("emul", allc)
+    return {"value": v_sh, "unit": "Gpixel-iter/s", "cores": hc["threads"],
+            "kind": "port", "value_1thread": v_1, "value_allcores": v_all, "cores_allcores": allc,
+            "value_emul": v_em, "value_emul_allcores": v_ema,
             "nproc": hc["nproc"], "affinity_cpus": hc["affinity"], "physical_cores": hc["physical_cores"],
-            "sample": f"oracle/gqmap_oracle.c fp64 ({engine}), {label} {No}x{Mo}, L={opts['L']} K={opts['K']}, "
-                      f"seeded init: {n_all} iterations on {hc['threads']} OpenMP threads in {t_all:.1f}s "
-                      f"(the process's CPU share: nproc {hc['nproc']}, affinity {hc['affinity']}, "
-                      f"OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS', 'unset')}), then {n_one} iterations "
-                      f"on 1 thread in {t_one:.1f}s"}
+            "sample": f"{label} {No}x{Mo} ({engine}, L={opts['L']} K={opts['K']}), seeded init, iterations from 1: "
+                      f"literal restatement oracle/gqmap_oracle.c fp64 -- {n_sh} its on {hc['threads']} OpenMP "
+                      f"threads in {t_sh:.1f}s (the process's CPU share: nproc {hc['nproc']}, affinity "
+                      f"{hc['affinity']}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS', 'unset')}), {n_1} on "
+                      f"1 thread in {t_1:.1f}s, {n_all} on {allc} threads (all physical cores) in {t_all:.1f}s; "
+                      f"CPU model of the kernel arithmetic oracle/gqmap_emul.cpp {precision} (bit-identical to the "
+                      f"GPU) -- {n_em} its on {hc['threads']} threads in {t_em:.1f}s, {n_ema} on {allc} in "
+                      f"{t_ema:.1f}s"}
+
+
+def parity_gate(r, engine, steps, precision, split, seed):
+    """The north-star gate (BASELINE.md:64-65), after the timed region: the
+    same `steps` iterations from the same seeded init on the CPU -- the CPU
+    model of the kernel arithmetic (oracle/gqmap_emul.cpp, must match the GPU
+    bit for bit: aepe_delta_emul == 0) and the literal restatement of the
+    reference (oracle/gqmap_oracle.c: aepe_delta_literal against the 1e-4
+    gate) -- then AEPE (gqmap_gpu_mixture.m:63-64) and flowToColor
+    (gqmap_gpu_mixture.m:60; uint8 pixels that differ) of each CPU flow
+    against the GPU's."""
+    from gqmap_opticalflow_amd import aepe, flow_to_color, gauss_hermite, initial_state
+    from oracle import oracle
+    I1, I2, opts, mp_gpu, flo, unk = r["I1"], r["I2"], r["opts"], r["map"], r["flo"], r["unk"]
+    Mo, No = I1.shape
+    sup = engine == "super"
+    M, N = (Mo // 4, No // 4) if sup else (Mo, No)
+    o = dict(opts, engine=engine)
+    L = int(o["L"])
+    X, W = gauss_hermite(int(o["K"]))
+    threads = allcore_threads(host_cpus())
+    up = (lambda f: np.repeat(np.repeat(f, 4, axis=0), 4, axis=1)) if sup else (lambda f: f)
+    crop = 4 if sup else 1
+
+    def cpu_map(st, det_exp):
+        if L == 1:
+            return np.stack([st.muu[:, :, 0], st.muv[:, :, 0]], axis=2)
+        return oracle.get_map(st.alpha, st.muu, st.sigu, st.muv, st.sigv, nthreads=threads, det_exp=det_exp)
+
+    def colour(f):
+        f = up(f)
+        return f[4:-4, 4:-4] if sup else f
+
+    img_gpu = flow_to_color(colour(mp_gpu))[0]
+    a_gpu = aepe(flo, up(mp_gpu), unk, crop)
+    out = {"its": steps, "threads": threads, "gate": 1e-4, "aepe_gpu": a_gpu}
+    for kind in ("emul", "literal"):
+        st0 = initial_state(o, M, N, seed=seed, engine=engine)
+        st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
+        t0 = time.perf_counter()
+        if kind == "emul":
+            done, _, _ = oracle.emu_run(o, I1, I2, st, 1, steps, X, W, T=st0.T, nthreads=threads,
+                                        fp32=precision == "fp32", split=split)
+        else:
+            done, _, _ = oracle.run(o, I1, I2, st, 1, steps, T=st0.T, nthreads=threads)
+        mp = cpu_map(st, det_exp=kind == "emul")
+        a = aepe(flo, up(mp), unk, crop)
+        img = oracle.flow_to_color(colour(mp))[0]
+        out[f"aepe_cpu_{kind}"] = a
+        out[f"aepe_delta_{kind}"] = a_gpu - a
+        out[f"colour_mismatch_{kind}"] = int(np.any(img != img_gpu, axis=2).sum())
+        out[f"flow_max_abs_diff_{kind}"] = float(np.max(np.abs(mp - mp_gpu)))
+        out[f"cpu_s_{kind}"] = time.perf_counter() - t0
+        if done != steps:
+            out[f"error_{kind}"] = f"stopped after {done}/{steps}"
+    out["flow_bit_exact_emul"] = out["flow_max_abs_diff_emul"] == 0.0
+    out["gate_pass_literal"] = abs(out["aepe_delta_literal"]) <= 1e-4
+    out["colour_pixels"] = int(img_gpu.shape[0] * img_gpu.shape[1])
+    out["note"] = ("emul: the CPU model sharing the kernel's arithmetic spec (gqmap_math.h) -- bit-exact at any "
+                   "number of iterations; literal: the fp64 restatement of the MATLAB, which differs by a rounding "
+                   "or two per operation -- the solver's transient is chaotic, so that difference grows with the "
+                   "iteration count (DESIGN.md 2)")
+    return out
 
 
 def traffic_per_launch(precision: str, config: str):
@@ -233,12 +317,13 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     else:
         a = aepe(flo, mp, unk)
     nodes = eng.M * eng.N
+    split = eng.info().split
     eng.close()
     Mo, No = I1.shape
     ksuf = {"mixture": 0, "super": 1}[engine]
     R = "double" if args.precision == "fp64" else "float"
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, instrumented_ms=total_ms, pixels=Mo * No, nodes=nodes, aepe=a, name=name,
-                I1=I1, I2=I2, opts=opts, Mo=Mo, No=No,
+                I1=I1, I2=I2, opts=opts, Mo=Mo, No=No, map=mp, flo=flo, unk=unk, split=split, seed=rank,
                 kernel=f"gq::k_iter<{R},float,{ksuf},Q> (VV stored as float: integer frames)",
                 workload=f"{label}: {name} {No}x{Mo} {engine} L={L} K={K} its={args.steps} "
                          f"(one step = one full-frame iteration)")
@@ -410,9 +495,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong-scaling", action="store_true",
                     help="c2: skip the strong-scaling leg (the pair split over the ranks)")
-    ap.add_argument("--cpu-allcores", action="store_true",
-                    help="add a CPU-baseline leg on every physical core (off by default: a GPU box grants "
-                         "each GPU a share of its cores through OMP_NUM_THREADS)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the parity gate (CPU model + literal restatement of the same steps, AEPE and "
+                         "colour deltas) after the timed region")
     ap.add_argument("--tiled", action="store_true",
                     help="c2: strong scaling -- the RubberWhale pair split into column strips over the ranks")
     args = ap.parse_args()
@@ -563,7 +648,7 @@ def main():
             if out is not None:
                 out["strong_scaling"] = {"error": f"no result within {limit:.0f} s (watchdog)"}
             emit()
-            os._exit(0)
+            os._exit(3)  # the line is out; a stuck exchange is still a failed run
         import threading
         wd = threading.Timer(limit, fire)
         wd.daemon = True
@@ -587,6 +672,17 @@ def main():
         except Exception as e:  # reported in the line; the frame-parallel value stands
             if out is not None:
                 out["strong_scaling"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if rank == 0 and "map" in r and not args.no_parity:
+        # the north-star parity gate on rank 0's own pair, after the timed region
+        try:
+            par = parity_gate(r, engine, args.steps, args.precision, r["split"], r["seed"])
+            out["parity"] = par
+            for k in ("aepe_cpu_emul", "aepe_cpu_literal", "aepe_delta_emul", "aepe_delta_literal"):
+                out[k] = par[k]
+            out["colour_mismatch"] = par["colour_mismatch_emul"]
+            out["colour_mismatch_literal"] = par["colour_mismatch_literal"]
+        except Exception as e:  # reported, never hides the measured line
+            out["parity"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the CPU baseline is a rank-0, N=1 figure (bench contract)
         if cfg == "c1":
@@ -597,7 +693,8 @@ def main():
             I1c, I2c, oc = r["I1"], r["I2"], r["opts"]
             if cfg == "c5":  # bounded sample: a 388x584 window of the upsampled frame
                 I1c, I2c = (np.asfortranarray(a[600:988, 900:1484]) for a in (I1c, I2c))
-            out["cpu_baseline"] = cpu_baseline(I1c, I2c, oc, engine, lab, allcores=args.cpu_allcores)
+            out["cpu_baseline"] = cpu_baseline(I1c, I2c, oc, engine if cfg != "c3" else "ctf", lab,
+                                               split=r.get("split"), precision=args.precision)
     emit()
     if dist is not None:
         dist.destroy_process_group()

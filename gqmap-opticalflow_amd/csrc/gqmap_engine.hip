@@ -1335,7 +1335,10 @@ constexpr int BAR_LINE = 32;  // unsigned words per 128-byte line: one counter p
 // rule (0: none).  Per iteration, not a flag: the finalizer may already be
 // writing finalize(j - 1)'s verdict while a slow workgroup still reads
 // finalize(j - 2)'s after barrier j - 1.
-constexpr int BAR_EXIT = 8 * BAR_LINE, BAR_FAIL = 9 * BAR_LINE, BAR_STOP = 10 * BAR_LINE, BAR_WORDS = 11 * BAR_LINE;
+// BAR_INJECT (tests only, gqmap_debug_persist_fault): j + 1 makes barrier j
+// of the next persistent launch fail as a timed-out one does.
+constexpr int BAR_EXIT = 8 * BAR_LINE, BAR_FAIL = 9 * BAR_LINE, BAR_STOP = 10 * BAR_LINE, BAR_INJECT = 11 * BAR_LINE,
+              BAR_WORDS = 12 * BAR_LINE;
 constexpr unsigned BAR_SPIN_LIMIT = 1u << 21;  // polls (~1 us each) before a barrier gives up
 
 // Arrival: every wave's stores (state, partial row) have completed, then one
@@ -1367,7 +1370,13 @@ __device__ __forceinline__ bool pbar_wait(unsigned *bar, int j, int nblk, int *s
             unsigned v = 0xffffffffu, f = 0;
             if (x < 8) v = __hip_atomic_load(bar + x * BAR_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else if (x == 8) f = __hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__any(f != 0)) { go = 0; break; }
+            else if (x == 9)  // injected failure of barrier j (tests): as a timeout below
+                f = __hip_atomic_load(bar + BAR_INJECT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(j + 1);
+            if (__any(f != 0)) {
+                if (x == 9 && f) __hip_atomic_store(bar + BAR_FAIL, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                go = 0;
+                break;
+            }
             if (__all(v >= need)) break;
             if (++spins > BAR_SPIN_LIMIT) {
                 if (x == 0) __hip_atomic_store(bar + BAR_FAIL, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1435,10 +1444,14 @@ void k_iter_persist(IterParams<R, VT> P, int n_iter)
     // nothing writes Ctl before the first barrier, which every workgroup
     // reaches only after these reads: all workgroups see the same values
     if (ctl->stop) return;
+    unsigned *bar = P.bar;
+    // a failed launch (this one, or an earlier one of the same replay): do
+    // nothing -- the host restores the chunk's snapshot (k_persist_snap) and
+    // re-runs it with one launch per iteration
+    if (__hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
     const int nblk = gridDim.x, G = nblk - 1, b = blockIdx.x;
     const int it0 = ctl->it, done0 = ctl->done;
     double T = ctl->T;
-    unsigned *bar = P.bar;
     __shared__ int sh_flag;
     if (b == G) {  // finalizer: finalize(j - 1) during iteration j
         __shared__ fix128 fsh[NFIX][8];
@@ -1480,6 +1493,26 @@ void k_iter_persist(IterParams<R, VT> P, int n_iter)
         if (P.fin.t_decay_every > 0 && it % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
     }
     pbar_exit(bar, nblk);
+}
+
+// Before every persistent launch: the state it starts from (the current
+// ping-pong buffer and Ctl), unless a launch has already failed -- then the
+// snapshot of the failed launch's start is kept for the host to restore.
+template <typename R>
+__global__ __launch_bounds__(256) void k_persist_snap(const Ctl *ctl, const unsigned *bar, const R *st0, const R *st1,
+                                                      R *snap, Ctl *snap_ctl, int64_t n)
+{
+    if (__hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    const R *cur = (ctl->done & 1) ? st1 : st0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        snap[i] = cur[i];
+    if (blockIdx.x == 0) {
+        constexpr int W = (int)(sizeof(Ctl) / sizeof(uint32_t));
+        static_assert(sizeof(Ctl) % sizeof(uint32_t) == 0, "Ctl words");
+        const uint32_t *a = reinterpret_cast<const uint32_t *>(ctl);
+        uint32_t *d = reinterpret_cast<uint32_t *>(snap_ctl);
+        for (int w = threadIdx.x; w < W; w += blockDim.x) d[w] = a[w];
+    }
 }
 
 __global__ __launch_bounds__(256) void k_finalize(FinParams F)
@@ -1733,6 +1766,12 @@ struct gqmap_ctx {
     Ctl *d_ctl = nullptr;
     fix128 *d_partials = nullptr;  // 2 x nblocks rows (k_iter_persist alternates halves)
     unsigned *d_bar = nullptr;      // k_iter_persist barrier counters (BAR_WORDS)
+    // k_iter_persist recovery: the state a launch starts from (k_persist_snap);
+    // after a failed launch the context runs one launch per iteration
+    void *d_snap = nullptr;
+    Ctl *d_snap_ctl = nullptr;
+    size_t snap_bytes = 0;
+    bool persist_off = false;
     double *d_trace = nullptr;
     double *d_truth = nullptr;  // gqmap_set_truth: M x N x 2 (ctf engine)
     size_t truth_elems = 0;     // doubles d_truth was allocated for
@@ -1743,6 +1782,9 @@ struct gqmap_ctx {
     int kq = 1;         // kernel shape: split, or 0 = role split (Q = 1 arithmetic, 16 x 8 tiles)
     int lpar = 1;       // k_iter blocks per tile (components spread over blocks)
     hipGraphExec_t graph = nullptr;
+    // graphs of 2^k iterations (k < SUB_GRAPHS) for the part of a run below
+    // GRAPH_CHUNK: every count runs as replayed graphs (gqmap_prepare builds them)
+    hipGraphExec_t sub[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     bool own_stream = true;
     double tab_host[NTAB * TS];
     // column-strip tiling (gqmap_create_tile): node columns [col0, col1) of Ng
@@ -1824,7 +1866,30 @@ size_t halo_bytes(const gqmap_ctx *c, int k)
     return (size_t)np * c->L * c->M * c->rsz;
 }
 
-gqmap_status alloc_grid(gqmap_ctx *c)
+// Column strip of tile c->tile of a Mo x No frame: the local node grid
+// (owned columns + one ghost column per neighbour).  No allocation.
+void strip_geometry(gqmap_ctx *c, int Mo, int No)
+{
+    const int M = c->super_ ? Mo / 4 : Mo, Ng = c->super_ ? No / 4 : No;
+    // column strip [col0, col1) + one ghost column per neighbour
+    const int col0 = (int)((int64_t)Ng * c->tile / c->n_tiles);
+    const int col1 = (int)((int64_t)Ng * (c->tile + 1) / c->n_tiles);
+    const int gl = c->tile > 0, gr = c->tile < c->n_tiles - 1;
+    c->Mo = Mo;
+    c->No = No;
+    c->M = M;
+    c->N = (col1 - col0) + gl + gr;
+    c->Ng = Ng;
+    c->col0 = col0;
+    c->col1 = col1;
+    c->n_off = col0 - gl;
+    c->own_lo = gl;
+    c->own_hi = gl + (col1 - col0);
+    c->MNL = (int64_t)c->M * c->N * c->L;
+}
+
+// Lanes per node, kernel shape and the tile grid of the local node grid.
+void tile_grid(gqmap_ctx *c)
 {
     // from the whole grid (Ng columns), so every column-strip tile sums its
     // quadrature in the same order as the untiled solve
@@ -1839,6 +1904,11 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     c->tiles_n = (c->N + tc - 1) / tc;
     c->lpar = choose_lpar(c);
     c->nblocks = c->tiles_m * c->tiles_n * c->lpar;
+}
+
+gqmap_status alloc_grid(gqmap_ctx *c)
+{
+    tile_grid(c);
     const size_t bytes = (size_t)c->MNL * NPLANES * c->rsz;
     for (int b = 0; b < 2; ++b) {
         if (c->d_st[b]) (void)hipFree(c->d_st[b]);
@@ -1850,6 +1920,43 @@ gqmap_status alloc_grid(gqmap_ctx *c)
     GQ_HIP(hipMalloc((void **)&c->d_partials, sizeof(fix128) * (size_t)2 * c->nblocks * (NFIX + c->L) + 64));
     return GQMAP_OK;
 }
+
+// A subset of the tiles for one k_iter launch (tile contexts: boundary tile
+// columns / interior), see IterParams::seg_lo.
+struct TileSegs {
+    int lo[2], n[2];
+    int part_off;
+};
+
+// The boundary tile columns of a column-strip tile (those holding its first
+// and last owned node columns: their results are what the neighbours need)
+// and the rest.  Together they cover every tile once; block partial rows
+// [0, bnd) and [bnd, nblocks).
+void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
+{
+    const int TN = tile_cols(c->kq);  // tile columns
+    const int tm = c->tiles_m, cb0 = c->own_lo / TN, cb1 = (c->own_hi - 1) / TN;
+    bnd.lo[0] = cb0 * tm; bnd.n[0] = tm;
+    bnd.lo[1] = cb1 * tm; bnd.n[1] = cb1 != cb0 ? tm : 0;
+    bnd.part_off = 0;
+    inr.lo[0] = (cb0 + 1) * tm; inr.n[0] = std::max(0, cb1 - cb0 - 1) * tm;
+    inr.lo[1] = (cb1 + 1) * tm; inr.n[1] = (c->tiles_n - cb1 - 1) * tm;
+    inr.part_off = (bnd.n[0] + bnd.n[1]) * c->lpar;
+    // tile columns before cb0 hold ghost columns only (one-column tiles,
+    // Q = 64, of a strip with a left neighbour): never launched
+}
+
+// Workgroups of one RCCL-tile iteration (the boundary and the interior
+// launch): the count the last-arrival ticket of tile_totals_tail waits for.
+// Not c->nblocks -- a ghost-only tile column is not launched.
+int iteration_blocks(const gqmap_ctx *c)
+{
+    TileSegs bnd, inr;
+    tile_segments(c, bnd, inr);
+    return (bnd.n[0] + bnd.n[1] + inr.n[0] + inr.n[1]) * c->lpar;
+}
+
+
 
 FinParams fin_params(const gqmap_ctx *c);
 
@@ -1896,7 +2003,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     // RCCL tiles: exact totals straight from the k_iter launches (no
     // k_reduce_local between the launches and the all-gather)
     P.tile_acc = c->comm != nullptr;
-    P.ticket_total = c->nblocks;
+    P.ticket_total = c->comm ? iteration_blocks(c) : c->nblocks;
     fix128 *gt = c->gbuf ? c->gbuf : c->d_gathered;
     P.tile_totals = gt ? gt + (size_t)c->tile * (NFIX + c->L) : nullptr;
     P.spec = c->spec_now ? 1 : 0;
@@ -1935,30 +2042,6 @@ int2 kernel_shape(K kern)
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     return make_int2(std::max(1, per_cu), std::max(8, cus));
-}
-
-// A subset of the tiles for one k_iter launch (tile contexts: boundary tile
-// columns / interior), see IterParams::seg_lo.
-struct TileSegs {
-    int lo[2], n[2];
-    int part_off;
-};
-
-// The boundary tile columns of a column-strip tile (those holding its first
-// and last owned node columns: their results are what the neighbours need)
-// and the rest.  Together they cover every tile once; block partial rows
-// [0, bnd) and [bnd, nblocks).
-void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
-{
-    const int TN = tile_cols(c->kq);  // tile columns
-    const int tm = c->tiles_m, cb0 = c->own_lo / TN, cb1 = (c->own_hi - 1) / TN;
-    bnd.lo[0] = cb0 * tm; bnd.n[0] = tm;
-    bnd.lo[1] = cb1 * tm; bnd.n[1] = cb1 != cb0 ? tm : 0;
-    bnd.part_off = 0;
-    inr.lo[0] = (cb0 + 1) * tm; inr.n[0] = std::max(0, cb1 - cb0 - 1) * tm;
-    inr.lo[1] = (cb1 + 1) * tm; inr.n[1] = (c->tiles_n - cb1 - 1) * tm;
-    inr.part_off = (bnd.n[0] + bnd.n[1]) * c->lpar;
-    // columns before cb0 would be ghosts only (own_lo <= 1 < TM): none
 }
 
 template <typename R, typename VT, int ENG, int Q>
@@ -2073,8 +2156,32 @@ int persist_capacity()
         // take one wave slot per SIMD each, as the API counts them
         if (Q == 64) per_cu = std::min(per_cu, 1);
         cap = std::max(0, per_cu) * std::max(0, cus);
+        // GQMAP_PERSIST_CAP=n: resident workgroups assumed (tests force the
+        // per-iteration path with a capacity too small for the grid)
+        if (const char *e = std::getenv("GQMAP_PERSIST_CAP")) cap = atoi(e);
     }
     return cap;
+}
+
+// The snapshot buffers of the persistent path (allocated outside a capture;
+// a capture without them keeps per-iteration launches)
+bool ensure_snap(gqmap_ctx *c)
+{
+    const size_t need = (size_t)c->MNL * NPLANES * c->rsz;
+    if (c->d_snap && c->snap_bytes == need) return true;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(c->stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+    if (c->d_snap) (void)hipFree(c->d_snap);
+    c->d_snap = nullptr;
+    c->snap_bytes = 0;
+    if (!c->d_snap_ctl && hipMalloc((void **)&c->d_snap_ctl, sizeof(Ctl)) != hipSuccess) return false;
+    if (hipMalloc(&c->d_snap, need) != hipSuccess) {
+        c->d_snap = nullptr;
+        return false;
+    }
+    c->snap_bytes = need;
+    return true;
 }
 
 template <typename R, typename VT, int Q>
@@ -2082,7 +2189,14 @@ bool launch_persist_q(gqmap_ctx *c, int n, bool dry)
 {
     const int G = c->nblocks;
     if (G + 1 > persist_capacity<R, VT, Q>()) return false;
+    if (!ensure_snap(c)) return false;
     if (dry) return true;
+    {
+        const int64_t n = (int64_t)c->MNL * NPLANES;
+        const int grid = (int)std::min<int64_t>((n + 255) / 256, 512);
+        k_persist_snap<R><<<grid, 256, 0, c->stream>>>(c->d_ctl, c->d_bar, (const R *)c->d_st[0],
+                                                       (const R *)c->d_st[1], (R *)c->d_snap, c->d_snap_ctl, n);
+    }
     IterParams<R, VT> P = iter_params<R, VT>(c);
     P.fused = 0;
     P.tile_acc = 0;
@@ -2117,7 +2231,7 @@ bool launch_persist_t(gqmap_ctx *c, int n, bool dry)
 bool launch_persist(gqmap_ctx *c, int n, bool dry = false)
 {
     static const bool off = std::getenv("GQMAP_NO_PERSIST") != nullptr;
-    if (off || c->opt.engine != GQMAP_ENGINE_CTF || c->L != 1 || c->n_tiles != 1 || c->comm || c->nranks != 0 ||
+    if (off || c->persist_off || c->opt.engine != GQMAP_ENGINE_CTF || c->L != 1 || c->n_tiles != 1 || c->comm || c->nranks != 0 ||
         !fused_finalize(c) || n < 1)
         return false;
     if (c->fp32) return launch_persist_t<float, float>(c, n, dry);
@@ -2312,15 +2426,15 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
 // stream in one order on every rank.  Totals of iteration j live in half
 // (j & 1) of d_gathered: half j & 1 is rewritten by iteration j + 2, which
 // starts after finalize(j).
-// Default: on when there are other ranks (a real collective to hide); behind
-// a one-rank communicator it measured no gain (profiles/r03_strip_spec.txt).
-// GQMAP_SPEC=1 / 0 forces it on / off (tests run it on one rank).
+// Opt-in (GQMAP_SPEC=1): behind a one-rank communicator it measured no gain
+// (profiles/r03_strip_spec.txt), and its cross-rank behaviour (ranks judging
+// the stop rule at different points of iteration j + 1) has not run with a
+// second GPU yet -- the default multi-rank step is launch_step_rccl.
 bool rccl_spec(const gqmap_ctx *c)
 {
     if (!c->comm || c->L != 1) return false;
     const char *e = std::getenv("GQMAP_SPEC");
-    if (e && *e) return *e == '1';
-    return c->n_tiles > 1;
+    return e && *e == '1';
 }
 
 template <typename R>
@@ -2422,21 +2536,39 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
     return st;
 }
 
+void drop_graph(gqmap_ctx *c);
+
 // A persistent launch whose grid barrier gave up (workgroups not all
-// resident, e.g. another kernel holding CUs) leaves the failure word set.
-gqmap_status check_persist(gqmap_ctx *c)
+// resident -- another process or stream holding CUs -- or descheduled past
+// the spin limit) leaves the failure word set; every later persistent
+// launch of the replay then returns at once, and the snapshot keeps the
+// state and Ctl the failed launch started from.  Recovery: restore that
+// snapshot (the failed launch may have half-written the other ping-pong
+// buffer and advanced Ctl part-way), clear the barrier words, and from here
+// on run this context with one launch per iteration (the graphs are
+// re-captured without the persistent launch).  *recovered: the run must go
+// on from the restored iteration.
+gqmap_status persist_recover(gqmap_ctx *c, bool *recovered)
 {
-    if (!launch_persist(c, 1, true)) return GQMAP_OK;
+    *recovered = false;
+    if (!c->d_snap) return GQMAP_OK;  // no persistent launch has run on this context
     unsigned f = 0;
     GQ_HIP(hipMemcpyAsync(&f, c->d_bar + BAR_FAIL, sizeof(f), hipMemcpyDeviceToHost, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
-    if (f != 0) {
-        GQ_HIP(hipMemsetAsync(c->d_bar, 0, sizeof(unsigned) * BAR_WORDS, c->stream));
-        GQ_HIP(hipStreamSynchronize(c->stream));
-        set_error("persistent iteration kernel: grid barrier timed out (%d workgroups not co-resident)",
-                  c->nblocks + 1);
-        return GQMAP_ERR_HIP;
-    }
+    if (f == 0) return GQMAP_OK;
+    Ctl h;
+    GQ_HIP(hipMemcpyAsync(&h, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    GQ_HIP(hipMemcpyAsync(c->d_st[h.done & 1], c->d_snap, c->snap_bytes, hipMemcpyDeviceToDevice, c->stream));
+    GQ_HIP(hipMemcpyAsync(c->d_ctl, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToDevice, c->stream));
+    GQ_HIP(hipMemsetAsync(c->d_bar, 0, sizeof(unsigned) * BAR_WORDS, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    if (std::getenv("GQMAP_PERSIST_VERBOSE"))
+        fprintf(stderr, "gqmap: persistent launch failed (%d workgroups); restored iteration %d, "
+                        "continuing with one launch per iteration\n", c->nblocks + 1, h.it);
+    c->persist_off = true;
+    drop_graph(c);
+    *recovered = true;
     return GQMAP_OK;
 }
 
@@ -2466,29 +2598,41 @@ gqmap_status read_ctl(gqmap_ctx *c, Ctl *h)
     return GQMAP_OK;
 }
 
-gqmap_status ensure_graph(gqmap_ctx *c)
+constexpr int SUB_GRAPHS = 6;  // 2^5 = 32 < GRAPH_CHUNK
+static_assert((1 << SUB_GRAPHS) > GRAPH_CHUNK, "sub graphs cover a chunk's remainder");
+
+// The graph of n iterations (captured once, replayed).
+gqmap_status capture_steps(gqmap_ctx *c, int n, hipGraphExec_t *out)
 {
-    if (c->graph) return GQMAP_OK;
-    (void)launch_persist(c, GRAPH_CHUNK, true);  // occupancy query outside the capture
+    if (*out) return GQMAP_OK;
+    (void)launch_persist(c, n, true);  // occupancy query, snapshot buffers: outside the capture
     hipGraph_t g;
     GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    gqmap_status st = launch_steps(c, GRAPH_CHUNK);
+    gqmap_status st = launch_steps(c, n);
     hipError_t ec = hipStreamEndCapture(c->stream, &g);
     if (st != GQMAP_OK) {
         if (ec == hipSuccess) (void)hipGraphDestroy(g);
         return st;
     }
     GQ_HIP(ec);
-    hipError_t e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+    hipError_t e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     GQ_HIP(e);
     return GQMAP_OK;
 }
 
+gqmap_status ensure_graph(gqmap_ctx *c) { return capture_steps(c, GRAPH_CHUNK, &c->graph); }
+
+gqmap_status ensure_sub_graph(gqmap_ctx *c, int k) { return capture_steps(c, 1 << k, &c->sub[k]); }
+
 void drop_graph(gqmap_ctx *c)
 {
     if (c->graph) (void)hipGraphExecDestroy(c->graph);
     c->graph = nullptr;
+    for (hipGraphExec_t &g : c->sub) {
+        if (g) (void)hipGraphExecDestroy(g);
+        g = nullptr;
+    }
 }
 
 template <typename R>
@@ -2539,24 +2683,9 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
     GQ_CHECK(M >= 3 && Ng >= 3, GQMAP_ERR_INVALID_ARG, "node grid %dx%d has no interior", M, Ng);
     GQ_CHECK(Ng >= c->n_tiles, GQMAP_ERR_INVALID_ARG, "%d node columns cannot feed %d tiles", Ng,
              c->n_tiles);
-    // column strip [col0, col1) + one ghost column per neighbour
-    const int col0 = (int)((int64_t)Ng * c->tile / c->n_tiles);
-    const int col1 = (int)((int64_t)Ng * (c->tile + 1) / c->n_tiles);
-    const int gl = c->tile > 0, gr = c->tile < c->n_tiles - 1;
-    const int N = (col1 - col0) + gl + gr;
     DeviceGuard dg(c->device);
     const bool resize = Mo != c->Mo || No != c->No || vv32 != c->vv32 || !c->d_VV;
-    c->Mo = Mo;
-    c->No = No;
-    c->M = M;
-    c->N = N;
-    c->Ng = Ng;
-    c->col0 = col0;
-    c->col1 = col1;
-    c->n_off = col0 - gl;
-    c->own_lo = gl;
-    c->own_hi = gl + (col1 - col0);
-    c->MNL = (int64_t)c->M * c->N * c->L;
+    strip_geometry(c, Mo, No);
     c->vv32 = vv32;
     if (resize) {
         drop_graph(c);
@@ -2947,9 +3076,15 @@ gqmap_status gqmap_get_state(gqmap_ctx *c, gqmap_state *st)
 static gqmap_status fetch_trace(gqmap_ctx *c, int it_before, int n, double *trace, double *aepe = nullptr)
 {
     if ((!trace && !aepe) || n <= 0) return GQMAP_OK;
+    // only the ring slots of these n iterations (one run of slots, or two
+    // when it wraps): a short run copies a few hundred bytes, not the ring
     std::vector<double> ring((size_t)TRACE_W * TRACE_CAP);
-    GQ_HIP(hipMemcpyAsync(ring.data(), c->d_trace, ring.size() * sizeof(double),
-                          hipMemcpyDeviceToHost, c->stream));
+    const int s0 = (it_before - 1) % TRACE_CAP, n0 = std::min(n, TRACE_CAP - s0);
+    GQ_HIP(hipMemcpyAsync(ring.data() + (size_t)TRACE_W * s0, c->d_trace + (size_t)TRACE_W * s0,
+                          sizeof(double) * TRACE_W * n0, hipMemcpyDeviceToHost, c->stream));
+    if (n > n0)
+        GQ_HIP(hipMemcpyAsync(ring.data(), c->d_trace, sizeof(double) * TRACE_W * (n - n0), hipMemcpyDeviceToHost,
+                              c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     for (int i = 0; i < n; ++i) {
         const int slot = (it_before + i - 1) % TRACE_CAP;
@@ -3029,24 +3164,33 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         const int chunk = std::min(n_iter - total, TRACE_CAP);
         int left = chunk;
         static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
-        if (left >= GRAPH_CHUNK && !no_graph) {
-            if ((s = ensure_graph(c)) != GQMAP_OK) return s;
+        if (!no_graph) {
+            // GRAPH_CHUNK-iteration graphs, then the remainder as graphs of
+            // 2^k iterations (a short run replays graphs too)
+            if (left >= GRAPH_CHUNK && (s = ensure_graph(c)) != GQMAP_OK) return s;
             while (left >= GRAPH_CHUNK) {
                 GQ_HIP(hipGraphLaunch(c->graph, c->stream));
                 left -= GRAPH_CHUNK;
             }
+            for (int k = SUB_GRAPHS - 1; k >= 0; --k)
+                if (left & (1 << k)) {
+                    if ((s = ensure_sub_graph(c, k)) != GQMAP_OK) return s;
+                    GQ_HIP(hipGraphLaunch(c->sub[k], c->stream));
+                }
+            left = 0;
         }
         if (left > 0 && (s = launch_steps(c, left)) != GQMAP_OK) return s;
         GQ_HIP(hipGetLastError());
+        bool recovered = false;
+        if ((s = persist_recover(c, &recovered)) != GQMAP_OK) return s;
         Ctl h;
         if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
-        if ((s = check_persist(c)) != GQMAP_OK) return s;
         const int ran = h.it - (h0.it + total);
         if ((s = fetch_trace(c, h0.it + total, ran, trace ? trace + 3 * total : nullptr,
                              aepe ? aepe + total : nullptr)) != GQMAP_OK)
             return s;
         total += ran;
-        if (h.stop || ran < chunk) break;
+        if (h.stop || (ran < chunk && !recovered)) break;
     }
     if (n_done) *n_done = total;
     return GQMAP_OK;
@@ -3111,9 +3255,53 @@ gqmap_status gqmap_prepare(gqmap_ctx *c)
     gqmap_status s = ensure_graph(c);
     if (s != GQMAP_OK) return s;
     GQ_HIP(hipGraphUpload(c->graph, c->stream));
+    for (int k = 0; k < SUB_GRAPHS; ++k) {
+        if ((s = ensure_sub_graph(c, k)) != GQMAP_OK) return s;
+        GQ_HIP(hipGraphUpload(c->sub[k], c->stream));
+    }
     GQ_HIP(hipStreamSynchronize(c->stream));
     return GQMAP_OK;
 }
+
+// Not in the public header (tests, no device needed): the launch geometry of
+// column-strip tile `tile` of n_tiles over a Mo x No frame -- out = {nblocks
+// (the whole local tile grid), iteration_blocks (the workgroups of one RCCL
+// iteration: boundary + interior launches), tiles_m, tiles_n, kernel shape}.
+int gqmap_debug_strip_launch(const gqmap_options *opt, int Mo, int No, int n_tiles, int tile, int out[5])
+{
+    if (!opt || !out || n_tiles < 1 || tile < 0 || tile >= n_tiles) return GQMAP_ERR_INVALID_ARG;
+    gqmap_ctx c;
+    c.opt = *opt;
+    c.super_ = opt->engine == GQMAP_ENGINE_SUPER;
+    c.L = opt->L;
+    c.n_tiles = n_tiles;
+    c.tile = tile;
+    strip_geometry(&c, Mo, No);
+    tile_grid(&c);
+    out[0] = c.nblocks;
+    out[1] = iteration_blocks(&c);
+    out[2] = c.tiles_m;
+    out[3] = c.tiles_n;
+    out[4] = c.kq;
+    return GQMAP_OK;
+}
+
+// Not in the public header (tests): barrier j of the context's next
+// persistent launch fails as a timed-out one does (j < 0: clears).
+gqmap_status gqmap_debug_persist_fault(gqmap_ctx *c, int j)
+{
+    clear_error();
+    GQ_CHECK(c, GQMAP_ERR_INVALID_ARG, "null context");
+    DeviceGuard dg(c->device);
+    const unsigned v = j < 0 ? 0u : (unsigned)(j + 1);
+    GQ_HIP(hipMemcpyAsync(c->d_bar + BAR_INJECT, &v, sizeof(v), hipMemcpyHostToDevice, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    return GQMAP_OK;
+}
+
+// Not in the public header (tests): 1 when the context has fallen back from
+// the persistent launch to one launch per iteration.
+int gqmap_debug_persist_off(const gqmap_ctx *c) { return c && c->persist_off ? 1 : 0; }
 
 gqmap_status gqmap_get_info(gqmap_ctx *c, gqmap_info *info)
 {
@@ -3521,7 +3709,7 @@ void gqmap_destroy(gqmap_ctx *c)
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace,
-                    c->d_truth, (void *)c->d_bar};
+                    c->d_truth, (void *)c->d_bar, c->d_snap, (void *)c->d_snap_ctl};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);

@@ -256,6 +256,17 @@ class Engine:
         return energy, ptdmu, ptdsig, T
 
 
+def log_p(eng: Engine, mp) -> float:
+    """profile_logP (gqmap_gpu_mixture.m:148-154; super: node_lp,
+    gqmap_gpuSuper_mix_entropy.m:152-169) in array form: np(M_,N_) + the
+    circshift edge potentials, numpy sums."""
+    M, N = mp.shape[:2]
+    ns, ms = np.meshgrid(np.arange(1, N + 1), np.arange(1, M + 1))
+    npot = eng.node_pot(mp[:, :, 0], mp[:, :, 1], ms, ns)
+    ep = sum(eng.edge_pot(mp, s) for s in (np.roll(mp, -1, axis=0), np.roll(mp, -1, axis=1)))
+    return float(npot[1:-1, 1:-1].sum() + ep[1:-1, 1:-1].sum())
+
+
 def projsplx(y):
     y = np.asarray(y, dtype=np.float64).ravel()
     m = y.size

@@ -633,6 +633,61 @@ double orc_aepe(const double *tflow, const double *flow, const unsigned char *un
     return s / (N - 2 * r0);
 }
 
+/* profile_logP (gqmap_gpu_mixture.m:148-154; super gqmap_gpuSuper_mix_entropy.m:
+ * 152-169).  map is the M x N x 2 MAP flow on the node grid.
+ *   np = arrayfun(@node_pot, us, vs, ms, ns)    (super: node_lp, the 4x4 block
+ *                                                sum of node_pot, :160-169)
+ *   ep = arrayfun(@edge_pot, cat(4,uv,uv), cat(4,circshift(uv,-1),circshift(uv,-1,2)))
+ *   lp = sum(sum(np(M_,N_))) + sum(sum(sum(sum(ep(M_,N_,:,:)))))
+ * with M_ = 2:M-1, N_ = 2:N-1.  MATLAB's sum order: down each column, then
+ * across the columns (ep: then over the uv and direction planes). */
+double orc_log_p(const orc_params *p, const double *I1, const double *VV, const double *map)
+{
+    orc_ctx c;
+    ctx_init(&c, p, I1, VV);
+    const int M = p->M, N = p->N;
+    const size_t MN = (size_t)M * N;
+    double snp = 0;
+    for (int n = 2; n <= N - 1; ++n) {  /* 1-based node columns */
+        double col = 0;
+        for (int m = 2; m <= M - 1; ++m) {
+            const size_t i = (m - 1) + (size_t)M * (n - 1);
+            const double x1 = map[i], x2 = map[MN + i];
+            double v;
+            if (p->super_) {
+                const int bottom = 4 * m, top = bottom - 3, right = 4 * n, left = right - 3;
+                v = 0;
+                for (int ii = top; ii <= bottom; ++ii)
+                    for (int jj = left; jj <= right; ++jj) v = v + node_pot(&c, x1, x2, ii, jj);
+            } else {
+                v = node_pot(&c, x1, x2, m, n);
+            }
+            col += v;
+        }
+        snp += col;
+    }
+    /* ep(:,:,uv,dir): dir 1 pairs (m,n) with circshift(uv,-1) = (m+1,n), dir 2
+     * with circshift(uv,-1,2) = (m,n+1) (wrapping, as circshift does) */
+    double sep = 0;
+    for (int dir = 0; dir < 2; ++dir) {
+        double sdir = 0;
+        for (int uv = 0; uv < 2; ++uv) {
+            double suv = 0;
+            for (int n = 1; n <= N - 2; ++n) {
+                double col = 0;
+                for (int m = 1; m <= M - 2; ++m) {
+                    const int m2 = dir == 0 ? (m + 1) % M : m, n2 = dir == 1 ? (n + 1) % N : n;
+                    col += edge_pot(&c, map[MN * uv + m + (size_t)M * n], map[MN * uv + m2 + (size_t)M * n2]);
+                }
+                suv += col;
+            }
+            sdir += suv;
+        }
+        sep += sdir;
+    }
+    return snp + sep;
+}
+
 /* ------------------------------------------------------------------ */
 /* Mixture MAP (findMixMax.m:39-70) with MATLAB fminbnd (Brent)         */
 /* ------------------------------------------------------------------ */

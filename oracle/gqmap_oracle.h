@@ -82,6 +82,10 @@ void orc_flow_to_color(const double *flow, int M, int N, double max_flow,
 double orc_aepe(const double *tflow, const double *flow, const unsigned char *unknown,
                 int M, int N, int r0);
 
+/* profile_logP (gqmap_gpu_mixture.m:148-154; super node_lp,
+ * gqmap_gpuSuper_mix_entropy.m:152-169) of the M x N x 2 MAP flow `map`. */
+double orc_log_p(const orc_params *p, const double *I1, const double *VV, const double *map);
+
 /* findMixMax.m:39-70 semantics: per pixel, best of component means vs
  * fminbnd (Brent, TolX=1e-4) on [min mu, max mu].  out [M*N*2]. */
 void orc_get_map(const double *alpha, const double *muu, const double *sigu,

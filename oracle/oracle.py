@@ -178,6 +178,22 @@ def gradients(opts: dict, I1, I2, state: State, T: float | None = None, nthreads
             edge.reshape((p.M, p.N, p.L, 2, 2, 7), order="F"))
 
 
+def log_p(opts: dict, I1, I2, mp) -> float:
+    """profile_logP (gqmap_gpu_mixture.m:148-154; super node_lp,
+    gqmap_gpuSuper_mix_entropy.m:152-169) of the M x N x 2 MAP flow mp."""
+    I1 = _f64(I1)
+    Mo, No = I1.shape
+    p = make_params(opts, Mo, No)
+    VV = get_vv(I2)
+    mp = _f64(mp)
+    if mp.shape != (p.M, p.N, 2):
+        raise ValueError(f"map shape {mp.shape} != node grid {(p.M, p.N, 2)}")
+    f = lib().orc_log_p
+    f.restype = C.c_double
+    f.argtypes = [C.POINTER(OrcParams), C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    return f(C.byref(p), _p(I1), _p(VV), _p(mp))
+
+
 def projsplx(y) -> np.ndarray:
     y = _f64(np.asarray(y, dtype=np.float64).ravel())
     x = np.zeros_like(y)

@@ -68,3 +68,77 @@ def test_persistent_stop_rule(split, where):
     for key in G.STATE_KEYS:
         np.testing.assert_array_equal(getattr(g, key), getattr(ref[2], key), err_msg=key)
     assert g.it == ref[2].it == st.it + k + 1
+
+
+@pytest.mark.parametrize("split", [8, 64])
+@pytest.mark.parametrize("barrier", [0, 7, 49])
+def test_persistent_failure_recovers_bit_exact(split, barrier):
+    # A persistent launch whose grid barrier gives up (workgroups not
+    # co-resident, or descheduled past the spin limit) is simulated by failing
+    # barrier `barrier` of the first launch (gqmap_debug_persist_fault): the
+    # run restores the snapshot the failed launch started from and goes on
+    # with one launch per iteration -- same trace, same state, same bits as
+    # an undisturbed run, and no error.
+    import ctypes as C
+    import dataclasses
+    from gqmap_opticalflow_amd import Engine, _lib
+    M, N = (60, 70) if split == 8 else (30, 44)
+    I1, I2, _, _, o, st = _reference_init_case("rubberwhale", M, N, 150, 200, L=1, K=11, engine="ctf",
+                                               split=split, t_decay_every=20)
+    o = dict(o, temperature=0.3)
+    st = dataclasses.replace(st, T=0.3)
+    its = 130
+    _, ref_tr, ref, _ = _run_engine(o, I1, I2, "ctf", "fp64", st, its)
+    lib = _lib.load()
+    lib.gqmap_debug_persist_fault.argtypes = [C.c_void_p, C.c_int]
+    lib.gqmap_debug_persist_off.argtypes = [C.c_void_p]
+    with Engine(o, I1, I2, "ctf", "fp64") as eng:
+        eng.set_state(st)
+        eng.prepare()  # graphs captured with the persistent launch
+        assert lib.gqmap_debug_persist_off(eng.ctx) == 0
+        assert lib.gqmap_debug_persist_fault(eng.ctx, barrier) == 0
+        done, tr = eng.run(its)
+        assert lib.gqmap_debug_persist_off(eng.ctx) == 1  # fell back
+        g = eng.get_state()
+        # and it keeps running correctly afterwards (per-iteration graphs)
+        done2, tr2 = eng.run(20)
+        g2 = eng.get_state()
+    assert done == its
+    np.testing.assert_array_equal(tr, ref_tr)
+    for key in G.STATE_KEYS:
+        np.testing.assert_array_equal(getattr(g, key), getattr(ref, key), err_msg=key)
+    assert g.it == ref.it and g.T == ref.T
+    _, tr3, ref2, _ = _run_engine(o, I1, I2, "ctf", "fp64", st, its + 20)
+    np.testing.assert_array_equal(tr2, tr3[its:])
+    for key in G.STATE_KEYS:
+        np.testing.assert_array_equal(getattr(g2, key), getattr(ref2, key), err_msg=key)
+
+
+def test_persistent_capacity_override_runs_per_iteration():
+    # GQMAP_PERSIST_CAP: a capacity too small for the grid keeps the level on
+    # one launch per iteration (the path a device without room takes) -- the
+    # same bits as the persistent launch
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, ".")
+from tests.test_gpu_parity import _reference_init_case, _run_engine
+I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 30, 44, 150, 200, L=1, K=11, engine="ctf", split=64)
+_, tr, g, _ = _run_engine(o, I1, I2, "ctf", "fp64", st, 70)
+np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigv.ravel(), g.rou.ravel()]))
+'''
+    import os
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as d:
+        outs = []
+        for cap in (None, "1"):
+            env = dict(os.environ)
+            env.pop("GQMAP_PERSIST_CAP", None)
+            if cap:
+                env["GQMAP_PERSIST_CAP"] = cap
+            f = os.path.join(d, f"r{cap}.npy")
+            subprocess.run([sys.executable, "-c", code, f], cwd=root, env=env, check=True, timeout=300)
+            outs.append(np.load(f))
+    np.testing.assert_array_equal(outs[0], outs[1])

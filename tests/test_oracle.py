@@ -164,3 +164,22 @@ def test_map_deterministic_exp_mode(oracle_lib):
     y = oracle_lib.get_map(a, mu, sg, mu, sg, det_exp=True)
     np.testing.assert_allclose(x, y, atol=1e-4)
     np.testing.assert_array_equal(oracle_lib.get_map(a, mu, sg, mu, sg), x)
+
+
+@pytest.mark.parametrize("name", ["mixture_L1", "mixture_L3_T", "super_L3"])
+def test_oracle_log_p_matches_numpy_restatement(oracle_lib, name):
+    # profile_logP (gqmap_gpu_mixture.m:148-154; super node_lp,
+    # gqmap_gpuSuper_mix_entropy.m:152-169): the C restatement against the
+    # independent array-form numpy one, on the golden frames with a MAP that
+    # crosses the border clamps (displacements up to several pixels)
+    from oracle import gqmap_np
+    d = G.load(name)
+    o = d["opts"]
+    ne = gqmap_np.Engine(o, d["I1"], d["I2"])
+    rng = np.random.default_rng(7)
+    mp = np.asfortranarray(rng.uniform(-6, 6, size=(ne.M, ne.N, 2)))
+    ref = gqmap_np.log_p(ne, mp)
+    assert oracle_lib.log_p(o, d["I1"], d["I2"], mp) == pytest.approx(ref, rel=1e-12)
+    # a smooth MAP (the typical case) as well
+    mp2 = np.asfortranarray(np.stack(np.meshgrid(np.linspace(-1, 2, ne.N), np.linspace(0.5, -1.5, ne.M)), axis=2))
+    assert oracle_lib.log_p(o, d["I1"], d["I2"], mp2) == pytest.approx(gqmap_np.log_p(ne, mp2), rel=1e-12)

@@ -184,3 +184,55 @@ def test_tiles_over_gloo_two_ranks(oracle_lib):
             glob[:, col0:col1] = owned[k_i]
         np.testing.assert_array_equal(glob, a, err_msg=k)
     np.testing.assert_array_equal(np.array(trace), tr[:, :2])
+
+
+def test_strip_split_mirrors_library_thresholds():
+    # engine.strip_split restates gqmap_engine.hip choose_split on one strip's
+    # node count; oracle.split_for restates it for a whole grid
+    from gqmap_opticalflow_amd import strip_split
+    from oracle import oracle
+    for M in (30, 60, 120, 240, 388, 480):
+        for N in (40, 80, 160, 320, 584, 640):
+            assert strip_split(M, N, 1) == oracle.split_for(M, N), (M, N)
+    assert strip_split(388, 584, 8) == 4 and strip_split(388, 584, 2) == 2 and strip_split(30, 40, 2) == 64
+
+
+@pytest.mark.parametrize("engine", ["mixture", "super"])
+def test_rccl_iteration_ticket_counts_launched_blocks(engine):
+    # The last-arrival ticket of an RCCL tile iteration (tile_totals_tail)
+    # must count the workgroups the boundary + interior launches actually run.
+    # One-column tiles (Q = 64) never launch the ghost-only tile column 0 of
+    # a strip with a left neighbour: the ticket must be nblocks - tiles_m there
+    # (round-3 advisor finding: it was nblocks, so the totals row was never
+    # written).  Host-only geometry (gqmap_debug_strip_launch), no device.
+    import ctypes as C
+    from gqmap_opticalflow_amd import _lib
+    from gqmap_opticalflow_amd.engine import make_options
+    lib = _lib.load()
+    f = lib.gqmap_debug_strip_launch
+    f.restype = C.c_int
+    f.argtypes = [C.POINTER(_lib.GqmapOptions), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
+    tile_cols = {64: 1, 16: 4, 8: 4, 4: 8, 2: 8, 1: 16, 0: 8}
+    sup = engine == "super"
+    cases = ([(120, 160, 2, 0), (120, 160, 3, 0), (480, 640, 4, 0), (120, 160, 2, 16)] if sup else
+             [(30, 40, 2, 0), (30, 40, 3, 64), (60, 80, 4, 0), (60, 80, 2, 64), (388, 584, 8, 4),
+              (388, 584, 2, 0), (240, 320, 4, 8), (120, 160, 5, 16), (388, 584, 3, -1)])
+    hit_wn = False
+    for Mo, No, n, split in cases:
+        o = make_options(dict(K=11 if sup else 9, L=3 if sup else 1, split=split, minu=-1, maxu=1, minv=-1, maxv=1),
+                         engine)
+        for t in range(n):
+            out = (C.c_int * 5)()
+            assert f(C.byref(o), Mo, No, n, t, out) == 0
+            nblocks, it_blocks, tm, tn, kq = list(out)
+            lpar = o.L if sup else 1
+            own_lo = int(t > 0)
+            # launched: every tile column from the one holding the first owned
+            # node column to the last tile column (a right ghost-only column
+            # runs, computing nothing)
+            assert it_blocks == (tn - own_lo // tile_cols[kq]) * tm * lpar, (Mo, No, n, t, split, list(out))
+            assert nblocks == tn * tm * lpar
+            if kq == 64 and t > 0:
+                hit_wn = True
+                assert it_blocks == nblocks - tm
+    assert sup or hit_wn
