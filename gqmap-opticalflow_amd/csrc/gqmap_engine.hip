@@ -76,56 +76,20 @@ __device__ __forceinline__ float gq_sqrt_dev(float x)
 
 #define GQ_HD __device__ __forceinline__
 #define GQ_SQRT(x) gq::gq_sqrt_dev(x)
-#ifndef GQ_EDGE_UNROLL_N
-#define GQ_EDGE_UNROLL_N 2
-#endif
-#ifndef GQ_NODE_UNROLL_N
-#define GQ_NODE_UNROLL_N 1
-#endif
-#ifndef GQ_VV16  // experiment: exact-integer frames stored as _Float16 instead of float (fp64 engine)
-#define GQ_VV16 0
-#endif
-#ifndef GQ_FIN_GROUP
-#define GQ_FIN_GROUP 1  // finalize: the NFIX fixed sums loaded together (fp32 C2 -2 us)
-#endif
-#ifndef GQ_EDGE_PK  // fp32: mirror-pair edge sums on packed float2 registers (bit-identical)
-#define GQ_EDGE_PK 1
-#endif
-#ifndef GQ_TAB_LDS
-#define GQ_TAB_LDS 1
-#endif
-#ifndef GQ_PHASE_MIX
-#define GQ_PHASE_MIX 1
-#endif
-#ifndef GQ_MIN_WAVES
-#define GQ_MIN_WAVES 1
-#endif
+#include "gqmap_tuning.h"
 #define GQ_STR2(x) #x
 #define GQ_PRAGMA_UNROLL(n) _Pragma(GQ_STR2(unroll n))
 #define GQ_UNROLL2 GQ_PRAGMA_UNROLL(GQ_EDGE_UNROLL_N)
-#ifndef GQ_PAIR_UNROLL_N
-#define GQ_PAIR_UNROLL_N 2
-#endif
 #define GQ_PAIR_UNROLL GQ_PRAGMA_UNROLL(GQ_PAIR_UNROLL_N)
 #define GQ_NODE_UNROLL GQ_PRAGMA_UNROLL(GQ_NODE_UNROLL_N)
 #define GQ_UNROLL_FULL _Pragma("unroll")
 #define GQ_UMUL24(a, b) __umul24((uint32_t)(a), (uint32_t)(b))
 #define GQ_FRACT(x) __builtin_amdgcn_fract(x)  // v_fract_f64
-#ifndef GQ_SUPER_WAVE_UNIFORM  // super engine: shared-window branch only when the whole wave can take it
-#define GQ_SUPER_WAVE_UNIFORM 0  // measured: wins early (VALU), loses mid-run (gather-bound): off
-#endif
-#if GQ_SUPER_WAVE_UNIFORM
-#define GQ_WAVE_ALL(x) __all(x)
-#endif
 #include "gqmap_math.h"
 
 namespace gq {
 
-#if GQ_VV16
-typedef _Float16 vvs_t;  // compact VV storage of the fp64 engine
-#else
-typedef float vvs_t;
-#endif
+typedef float vvs_t;  // VV storage of the fp64 engine for integer-valued frames (exact)
 
 constexpr int TILE = 16;
 constexpr int BLOCK = TILE * TILE;
@@ -537,18 +501,6 @@ __device__ void fin_apply(const FinParams &F, const double *tot)
 // 2-wave (<= 256 VGPR) schedule.  GQ_MIN_WAVES / GQ_SUPER_WAVES: experiments.
 // smallest lanes-per-node split whose edge jobs prefetch the next job's
 // operands / run fully unrolled (experiments: GQ_PREFETCH_MIN_Q, GQ_UNROLL_MIN_Q)
-#ifndef GQ_PREFETCH_MIN_Q
-#define GQ_PREFETCH_MIN_Q 2
-#endif
-#ifndef GQ_UNROLL_MIN_Q
-#define GQ_UNROLL_MIN_Q 2
-#endif
-#ifndef GQ_SUPER_WAVES
-#define GQ_SUPER_WAVES 1
-#endif
-#ifndef GQ_MIDQ_WAVES  // single-pixel engines at Q = 2, 4, 8: waves/SIMD the allocation must allow
-#define GQ_MIDQ_WAVES 1
-#endif
 constexpr int min_waves(int eng, int q)
 {
     return GQ_MIN_WAVES > 1 ? GQ_MIN_WAVES
@@ -611,9 +563,6 @@ struct TileLds {
 template <typename R, int Q>
 using TileLdsQ = TileLds<R, tile_pix(Q), (Q > 1 && GQ_TAB_LDS), Q == 0>;
 
-#ifndef GQ_TIMELINE
-#define GQ_TIMELINE 0
-#endif
 #if GQ_TIMELINE
 // debug builds: per-block stamps (s_memrealtime, 100 MHz) of k_iter
 // iterations GQ_TIMELINE and GQ_TIMELINE + 1 (gqmap_debug_timeline), 16 words
@@ -647,28 +596,16 @@ __device__ __forceinline__ bool node_interior(const IterParams<R, VT> &P, int mm
 // L1 bypassed on the consumer -- so no L2 write-back / invalidate is needed
 // between its iterations.  Otherwise plain accesses (kernel boundaries order
 // them).
-#ifndef GQ_PERSIST_PLAIN  // timing experiment only (stale reads): plain state accesses in k_iter_persist
-#define GQ_PERSIST_PLAIN 0
-#endif
-#ifndef GQ_PERSIST_NOFIN  // timing experiment only (no trace / stop): the finalizer only arrives
-#define GQ_PERSIST_NOFIN 0
-#endif
-#ifndef GQ_PERSIST_Q4
-#define GQ_PERSIST_Q4 0
-#endif
-#ifndef GQ_PERSIST_SLEEP
-#define GQ_PERSIST_SLEEP 2
-#endif
 template <bool COH, typename R>
 __device__ __forceinline__ R ld_state(const R *p)
 {
-    if constexpr (COH && !GQ_PERSIST_PLAIN) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else return *p;
 }
 template <bool COH, typename R>
 __device__ __forceinline__ void st_state(R *p, R v)
 {
-    if constexpr (COH && !GQ_PERSIST_PLAIN) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
 }
 
@@ -1459,7 +1396,6 @@ void k_iter_persist(IterParams<R, VT> P, int n_iter)
         for (int j = 0; j <= n_iter; ++j) {
             if (j > 0) {
                 if (!pbar_wait(bar, j - 1, nblk, &sh_flag)) break;
-                if (GQ_PERSIST_NOFIN) { if (j < n_iter) pbar_arrive(bar); continue; }
                 pfin_reduce(P.fin, ((j - 1) & 1) * G, G, tot, fsh);
                 if (threadIdx.x == 0) {
                     fin_apply(P.fin, tot);
@@ -2735,7 +2671,7 @@ gqmap_status ctx_set_images_device(gqmap_ctx *c, const double *dI1, const double
     GQ_HIP(pad_vv_device(dI2, Mo, No, d_scratch, c->stream));
     const size_t nvv = (size_t)(Mo + 2) * (No + 2);
     bool vv32 = c->fp32;
-    if (!vv32 && !std::getenv("GQMAP_VV64") && !GQ_VV16)
+    if (!vv32 && !std::getenv("GQMAP_VV64"))
         GQ_HIP(f32_exact_device(d_scratch, nvv, d_flag, &vv32, c->stream));
     gqmap_status s = prepare_images(c, Mo, No, vv32);
     if (s != GQMAP_OK) return s;

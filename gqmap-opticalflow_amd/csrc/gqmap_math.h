@@ -180,10 +180,6 @@ GQ_HD void keys4(R t, R &w0, R &w1, R &w2, R &w3)
 #define GQ_FRACT(x) ((x) - floor(x))
 #endif
 
-#ifndef GQ_WAVE_ALL  // device: the predicate over the lanes of the wave; host: the lane's own
-#define GQ_WAVE_ALL(x) (x)
-#endif
-
 #ifndef GQ_UMUL24  // 24-bit multiply (full rate on the device; both factors < 2^24)
 #define GQ_UMUL24(a, b) ((uint32_t)(a) * (uint32_t)(b))
 #endif
@@ -208,17 +204,9 @@ GQ_HD VP elem_ptr(VP VV, uint32_t elem)
 template <typename R, typename VP>
 GQ_HD R bicubic_w4(VP VV, uint32_t o, uint32_t M2, R s0, R s1, R s2, R s3, R t0, R t1, R t2, R t3)
 {
-#ifdef GQ_ABL_NOGATHER  // timing ablation only: no memory traffic for the taps
-    const R a0 = t0 + s1, a1 = t1 * s2, a2 = t2 - s3, a3 = t3 + s0;
-    return fma(s3, a3, fma(s2, a2, fma(s1, a1, s0 * a0))) + (R)o * R(1e-30);
-#else
-    // taps are converted to R exactly (VV storage: double, or float / half when exact)
+    // taps are converted to R exactly (VV storage: double, or float when exact)
     constexpr uint32_t E = (uint32_t)sizeof(*VV);
-#ifdef GQ_ABL_UNIFORM  // timing ablation only: every lane gathers the same cell (one line per load)
-    const uint32_t ob = (o & 1u) * E, cb = M2 * E;
-#else
     const uint32_t ob = o * E, cb = M2 * E;  // byte offsets: cell, column stride
-#endif
     const auto c0 = byte_ptr(VV, ob);
     const R v0 = fma(R(c0[3]), t3, fma(R(c0[2]), t2, fma(R(c0[1]), t1, R(c0[0]) * t0)));
     const auto c1 = byte_ptr(VV, ob + cb);
@@ -228,7 +216,6 @@ GQ_HD R bicubic_w4(VP VV, uint32_t o, uint32_t M2, R s0, R s1, R s2, R s3, R t0,
     const auto c3 = byte_ptr(VV, ob + 3 * cb);
     const R v3 = fma(R(c3[3]), t3, fma(R(c3[2]), t2, fma(R(c3[1]), t1, R(c3[0]) * t0)));
     return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0)));
-#endif
 }
 
 // 4 x the Keys interpolation in the cell whose first tap is element o, at
@@ -388,11 +375,9 @@ GQ_HD R super_block_sum(VP VV, int M2, int Mo, int No, int i0, int j0, R x1, R x
                         const R (&I)[16])
 {
     // Both branches compute every output from the same cells, fractions and
-    // fma sequence, so the choice never changes a result (GQ_WAVE_ALL: the
-    // device may take the shared window only when the whole wave can --
-    // measured neutral on C4: a VALU win early in a run, a gather loss later).
-    const bool safe = GQ_WAVE_ALL(R(j0 + 1) + x1 >= R(1) && R(j0 + 4) + x1 <= R(No - 1) &&
-                                  R(i0 + 1) + x2 >= R(1) && R(i0 + 4) + x2 <= R(Mo - 1));
+    // fma sequence, so the choice never changes a result.
+    const bool safe = R(j0 + 1) + x1 >= R(1) && R(j0 + 4) + x1 <= R(No - 1) && R(i0 + 1) + x2 >= R(1) &&
+                      R(i0 + 4) + x2 <= R(Mo - 1);
     R f = 0;
     if (safe) {
         const R fx = floor(x1), fy = floor(x2);
