@@ -95,6 +95,18 @@ def host_cpus():
         avail = nproc
     omp = os.environ.get("OMP_NUM_THREADS")
     threads = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
+    quota = None  # CPUs' worth of time the cgroup grants (cpu.max quota / period)
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            parts = open(path).read().split()
+            if path.endswith("cpu.max") and parts and parts[0] != "max":
+                quota = int(parts[0]) / int(parts[1])
+            elif path.endswith("quota_us") and int(parts[0]) > 0:
+                quota = int(parts[0]) / int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        except (OSError, ValueError, IndexError, ZeroDivisionError):
+            continue
+        if quota:
+            break
     phys = set()
     try:
         pid = cid = None
@@ -109,7 +121,8 @@ def host_cpus():
                 pid = cid = None
     except OSError:
         pass
-    return {"nproc": nproc, "affinity": avail, "threads": threads, "physical_cores": len(phys) or None}
+    return {"nproc": nproc, "affinity": avail, "threads": threads, "physical_cores": len(phys) or None,
+            "cpu_quota": quota}
 
 
 def _timed_leg(run_n, budget_s):
@@ -177,6 +190,10 @@ def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 6.0
             "kind": "port", "value_1thread": v_1, "value_allcores": v_all, "cores_allcores": allc,
             "value_emul": v_em, "value_emul_allcores": v_ema,
             "nproc": hc["nproc"], "affinity_cpus": hc["affinity"], "physical_cores": hc["physical_cores"],
+            "cgroup_cpu_quota": hc["cpu_quota"],
+            "allcores_note": "the all-physical-core legs oversubscribe when the box's cgroup grants fewer CPUs than "
+                             "there are cores (cgroup_cpu_quota; OMP_NUM_THREADS names the share): `value` is the "
+                             "share's figure",
             "sample": f"{label} {No}x{Mo} ({engine}, L={opts['L']} K={opts['K']}), seeded init, iterations from 1: "
                       f"literal restatement oracle/gqmap_oracle.c fp64 -- {n_sh} its on {hc['threads']} OpenMP "
                       f"threads in {t_sh:.1f}s (the process's CPU share: nproc {hc['nproc']}, affinity "
@@ -205,7 +222,7 @@ def parity_gate(r, engine, steps, precision, split, seed):
     o = dict(opts, engine=engine)
     L = int(o["L"])
     X, W = gauss_hermite(int(o["K"]))
-    threads = allcore_threads(host_cpus())
+    threads = host_cpus()["threads"]
     up = (lambda f: np.repeat(np.repeat(f, 4, axis=0), 4, axis=1)) if sup else (lambda f: f)
     crop = 4 if sup else 1
 
@@ -240,9 +257,18 @@ def parity_gate(r, engine, steps, precision, split, seed):
         out[f"cpu_s_{kind}"] = time.perf_counter() - t0
         if done != steps:
             out[f"error_{kind}"] = f"stopped after {done}/{steps}"
+    if "map1" in r:  # per-step agreement: iteration 1 alone, GPU vs the literal restatement
+        st0 = initial_state(o, M, N, seed=seed, engine=engine)
+        st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
+        oracle.run(o, I1, I2, st, 1, 1, T=st0.T, nthreads=threads)
+        mp1 = cpu_map(st, det_exp=False)
+        out["it1_flow_max_abs_diff_literal"] = float(np.max(np.abs(mp1 - r["map1"])))
+        out["it1_aepe_delta_literal"] = aepe(flo, up(r["map1"]), unk, crop) - aepe(flo, up(mp1), unk, crop)
     out["flow_bit_exact_emul"] = out["flow_max_abs_diff_emul"] == 0.0
     out["gate_pass_literal"] = abs(out["aepe_delta_literal"]) <= 1e-4
     out["colour_pixels"] = int(img_gpu.shape[0] * img_gpu.shape[1])
+    out["colour_note"] = ("flowToColor scales every pixel by the frame's largest flow magnitude "
+                          "(flowToColor.m:66-70): one differing pixel can change the whole encoding")
     out["note"] = ("emul: the CPU model sharing the kernel's arithmetic spec (gqmap_math.h) -- bit-exact at any "
                    "number of iterations; literal: the fp64 restatement of the MATLAB, which differs by a rounding "
                    "or two per operation -- the solver's transient is chaotic, so that difference grows with the "
@@ -311,6 +337,18 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     done2, total_ms, kernel_ms = eng.run_timed(args.steps)
     if done2 != args.steps or not np.array_equal(eng.map(), mp):
         raise RuntimeError(f"rank {rank}: the instrumented replay differs from the timed run")
+    eng.init_state(seed=rank)  # iteration 1 alone (the parity gate's per-step agreement)
+    eng.run(1)
+    mp1 = eng.map()
+    # the parity gate compares the GPU flow after gate_its iterations with
+    # the CPU paths' (all the timed steps, unless the CPU would take minutes:
+    # the super engine's CPU model runs ~1 s per C4 iteration)
+    gate_its = min(args.steps, args.parity_steps or (args.steps if engine != "super" else 20))
+    mpg = mp
+    if gate_its != args.steps:
+        eng.init_state(seed=rank)
+        eng.run(gate_its)
+        mpg = eng.map()
     if engine == "super":
         flow = np.repeat(np.repeat(mp, 4, axis=0), 4, axis=1)
         a = aepe(flo, flow, unk, 4)
@@ -323,7 +361,7 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     ksuf = {"mixture": 0, "super": 1}[engine]
     R = "double" if args.precision == "fp64" else "float"
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, instrumented_ms=total_ms, pixels=Mo * No, nodes=nodes, aepe=a, name=name,
-                I1=I1, I2=I2, opts=opts, Mo=Mo, No=No, map=mp, flo=flo, unk=unk, split=split, seed=rank,
+                I1=I1, I2=I2, opts=opts, Mo=Mo, No=No, map=mpg, gate_its=gate_its, map1=mp1, flo=flo, unk=unk, split=split, seed=rank,
                 kernel=f"gq::k_iter<{R},float,{ksuf},Q> (VV stored as float: integer frames)",
                 workload=f"{label}: {name} {No}x{Mo} {engine} L={L} K={K} its={args.steps} "
                          f"(one step = one full-frame iteration)")
@@ -373,7 +411,8 @@ def run_c1(args, rank, world, local, barrier):
     elapsed = time.perf_counter() - t0
     M, N, _ = flo.shape
     err = float(np.sqrt(((mu - flo) ** 2).sum(axis=2))[~unk].mean())
-    return dict(elapsed=elapsed, pixels=M * N, nodes=M * N, aepe=err, flow=flo, opts=o, Mo=M, No=N, its=tr.shape[0],
+    return dict(elapsed=elapsed, pixels=M * N, nodes=M * N, aepe=err, flow=flo, unk=unk, mu=mu, opts=o, Mo=M, No=N,
+                its=tr.shape[0],
                 workload=f"C1: {name} {N}x{M} legacy/gqmap_cpu.m flow denoising (input = GT flow, unknowns 0), "
                          f"K=9, var=gama=1, dta=inf, {args.steps} its, sigma0 = U+2 (seed 0); value includes the "
                          f"call's host<->device copies; aepe = mean |mu - flow|")
@@ -390,17 +429,47 @@ def cpu_baseline_c1(flow, opts, budget_s: float = 8.0):
     X, W = gauss_hermite(9)
     sg0 = np.asfortranarray(np.full((M, N, 2), 2.5))
     legs = {}
-    for threads in (hc["threads"], 1):
+    allc = allcore_threads(hc)
+    for threads in (hc["threads"], 1, allc):
         def run_n(n, threads=threads):
             return oracle.cpu_run(dict(opts, its=n, min_its=10 ** 9), flow, sg0, X, W, nthreads=threads)[3].shape[0]
         legs[threads] = _timed_leg(run_n, budget_s)
-    (n_all, t_all), (n_one, t_one) = legs[hc["threads"]], legs[1]
+    (n_all, t_all), (n_one, t_one), (n_pc, t_pc) = legs[hc["threads"]], legs[1], legs[allc]
     return {"value": M * N * n_all / t_all / 1e9, "unit": "Gpixel-iter/s", "cores": hc["threads"], "kind": "port",
-            "value_1thread": M * N * n_one / t_one / 1e9, "nproc": hc["nproc"],
+            "value_1thread": M * N * n_one / t_one / 1e9, "value_allcores": M * N * n_pc / t_pc / 1e9,
+            "cores_allcores": allc, "nproc": hc["nproc"], "cgroup_cpu_quota": hc["cpu_quota"],
             "affinity_cpus": hc["affinity"], "physical_cores": hc["physical_cores"],
             "sample": f"oracle/gqmap_legacy_oracle.c fp64, {N}x{M}, K=9: {n_all} iterations on {hc['threads']} "
                       f"OpenMP threads (rows, as the reference parfor) in {t_all:.1f}s, {n_one} on 1 thread "
                       f"in {t_one:.1f}s"}
+
+
+def parity_gate_c1(r, steps):
+    """The north-star gate on the path it names, legacy/gqmap_cpu.m (config
+    C1): the C restatement (oracle/gqmap_legacy_oracle.c) from the same
+    sigma0 (U + 2, the library RNG, seed 0) for the same iterations; AEPE of
+    each result against the input flow (known pixels) and the uint8
+    flowToColor encoding of both (mismatching pixels)."""
+    from gqmap_opticalflow_amd import flow_to_color, gauss_hermite, rand_uniform
+    from oracle import oracle
+    flo, unk, mu = r["flow"], r["unk"], r["mu"]
+    M, N, _ = flo.shape
+    sg0 = np.asfortranarray(rand_uniform(0, 3, 2 * M * N).reshape((M, N, 2), order="F") + 2)
+    X, W = gauss_hermite(9)
+    t0 = time.perf_counter()
+    mu_c, _, _, tr = oracle.cpu_run(dict(r["opts"], its=steps), flo, sg0, X, W, nthreads=host_cpus()["threads"])
+    cpu_s = time.perf_counter() - t0
+    err = lambda m: float(np.sqrt(((m - flo) ** 2).sum(axis=2))[~unk].mean())
+    a_g, a_c = err(mu), err(mu_c)
+    img_g = flow_to_color(mu)[0]
+    img_c = oracle.flow_to_color(mu_c)[0]
+    mism = int(np.any(img_g != img_c, axis=2).sum())
+    return {"its": steps, "cpu_its": int(tr.shape[0]), "gate": 1e-4, "aepe_gpu": a_g, "aepe_cpu_literal": a_c,
+            "aepe_delta_literal": a_g - a_c, "flow_max_abs_diff_literal": float(np.max(np.abs(mu - mu_c))),
+            "colour_mismatch_literal": mism, "colour_pixels": M * N, "gate_pass_literal": abs(a_g - a_c) <= 1e-4,
+            "cpu_s_literal": cpu_s,
+            "note": "legacy/gqmap_cpu.m (the north star's named CPU path): the device engine is plain fp64 in the "
+                    "restatement's operation order, so the flows are bit-identical"}
 
 
 def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts):
@@ -495,6 +564,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-strong-scaling", action="store_true",
                     help="c2: skip the strong-scaling leg (the pair split over the ranks)")
+    ap.add_argument("--parity-steps", type=int, default=0,
+                    help="iterations of the parity gate (default: all timed steps; C4: 20)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the parity gate (CPU model + literal restatement of the same steps, AEPE and "
                          "colour deltas) after the timed region")
@@ -672,10 +743,19 @@ def main():
         except Exception as e:  # reported in the line; the frame-parallel value stands
             if out is not None:
                 out["strong_scaling"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if rank == 0 and cfg == "c1" and not args.no_parity:
+        try:
+            par = parity_gate_c1(r, r["its"])
+            out["parity"] = par
+            for k in ("aepe_cpu_literal", "aepe_delta_literal"):
+                out[k] = par[k]
+            out["colour_mismatch"] = par["colour_mismatch_literal"]
+        except Exception as e:
+            out["parity"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and "map" in r and not args.no_parity:
         # the north-star parity gate on rank 0's own pair, after the timed region
         try:
-            par = parity_gate(r, engine, args.steps, args.precision, r["split"], r["seed"])
+            par = parity_gate(r, engine, r["gate_its"], args.precision, r["split"], r["seed"])
             out["parity"] = par
             for k in ("aepe_cpu_emul", "aepe_cpu_literal", "aepe_delta_emul", "aepe_delta_literal"):
                 out[k] = par[k]

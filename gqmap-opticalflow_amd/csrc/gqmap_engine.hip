@@ -1709,6 +1709,11 @@ struct gqmap_ctx {
     size_t snap_bytes = 0;
     bool persist_off = false;
     double *d_trace = nullptr;
+    // pinned host mirrors: Ctl, the trace ring and the persistent failure
+    // word, read back together at the end of a run chunk (one sync)
+    Ctl *h_ctl = nullptr;
+    double *h_ring = nullptr;
+    unsigned *h_fail = nullptr;
     double *d_truth = nullptr;  // gqmap_set_truth: M x N x 2 (ctf engine)
     size_t truth_elems = 0;     // doubles d_truth was allocated for
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
@@ -2529,9 +2534,37 @@ gqmap_status upload_ctl(gqmap_ctx *c, int it, double T, const double *w, const d
 
 gqmap_status read_ctl(gqmap_ctx *c, Ctl *h)
 {
-    GQ_HIP(hipMemcpyAsync(h, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
+    *h = *c->h_ctl;
     return GQMAP_OK;
+}
+
+// Queue the copy of the trace-ring slots of iterations [it_first, it_first + n)
+// into the pinned mirror (one run of slots, two when it wraps).
+gqmap_status queue_trace(gqmap_ctx *c, int it_first, int n)
+{
+    if (n <= 0) return GQMAP_OK;
+    n = std::min(n, TRACE_CAP);
+    const int s0 = (it_first - 1) % TRACE_CAP, n0 = std::min(n, TRACE_CAP - s0);
+    GQ_HIP(hipMemcpyAsync(c->h_ring + (size_t)TRACE_W * s0, c->d_trace + (size_t)TRACE_W * s0,
+                          sizeof(double) * TRACE_W * n0, hipMemcpyDeviceToHost, c->stream));
+    if (n > n0)
+        GQ_HIP(hipMemcpyAsync(c->h_ring, c->d_trace, sizeof(double) * TRACE_W * (n - n0), hipMemcpyDeviceToHost,
+                              c->stream));
+    return GQMAP_OK;
+}
+
+// Iterations [it_first, it_first + n) of the pinned ring into the caller's
+// trace (Energy, ptdmu, ptdsigma) and aepe arrays.
+void copy_trace(const gqmap_ctx *c, int it_first, int n, double *trace, double *aepe)
+{
+    for (int i = 0; i < n; ++i) {
+        const int slot = (it_first + i - 1) % TRACE_CAP;
+        if (trace)
+            for (int q = 0; q < 3; ++q) trace[3 * i + q] = c->h_ring[TRACE_W * slot + q];
+        if (aepe) aepe[i] = c->h_ring[TRACE_W * slot + 3];
+    }
 }
 
 constexpr int SUB_GRAPHS = 6;  // 2^5 = 32 < GRAPH_CHUNK
@@ -2861,7 +2894,10 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
     if (hipMalloc(&c->d_tab, NTAB * TS * c->rsz) != hipSuccess ||
         hipMalloc((void **)&c->d_ctl, sizeof(Ctl)) != hipSuccess ||
         hipMalloc((void **)&c->d_trace, sizeof(double) * TRACE_W * TRACE_CAP) != hipSuccess ||
-        hipMalloc((void **)&c->d_bar, sizeof(unsigned) * BAR_WORDS) != hipSuccess) {
+        hipMalloc((void **)&c->d_bar, sizeof(unsigned) * BAR_WORDS) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_ctl, sizeof(Ctl), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_ring, sizeof(double) * TRACE_W * TRACE_CAP, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_fail, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
         set_error("device allocation failed");
         return fail(GQMAP_ERR_OUT_OF_MEMORY);
     }
@@ -3012,22 +3048,12 @@ gqmap_status gqmap_get_state(gqmap_ctx *c, gqmap_state *st)
 static gqmap_status fetch_trace(gqmap_ctx *c, int it_before, int n, double *trace, double *aepe = nullptr)
 {
     if ((!trace && !aepe) || n <= 0) return GQMAP_OK;
-    // only the ring slots of these n iterations (one run of slots, or two
-    // when it wraps): a short run copies a few hundred bytes, not the ring
-    std::vector<double> ring((size_t)TRACE_W * TRACE_CAP);
-    const int s0 = (it_before - 1) % TRACE_CAP, n0 = std::min(n, TRACE_CAP - s0);
-    GQ_HIP(hipMemcpyAsync(ring.data() + (size_t)TRACE_W * s0, c->d_trace + (size_t)TRACE_W * s0,
-                          sizeof(double) * TRACE_W * n0, hipMemcpyDeviceToHost, c->stream));
-    if (n > n0)
-        GQ_HIP(hipMemcpyAsync(ring.data(), c->d_trace, sizeof(double) * TRACE_W * (n - n0), hipMemcpyDeviceToHost,
-                              c->stream));
+    // only the ring slots of these n iterations: a short run copies a few
+    // hundred bytes, not the ring
+    gqmap_status s = queue_trace(c, it_before, n);
+    if (s != GQMAP_OK) return s;
     GQ_HIP(hipStreamSynchronize(c->stream));
-    for (int i = 0; i < n; ++i) {
-        const int slot = (it_before + i - 1) % TRACE_CAP;
-        if (trace)
-            for (int q = 0; q < 3; ++q) trace[3 * i + q] = ring[TRACE_W * slot + q];
-        if (aepe) aepe[i] = ring[TRACE_W * slot + 3];
-    }
+    copy_trace(c, it_before, n, trace, aepe);
     return GQMAP_OK;
 }
 
@@ -3117,14 +3143,22 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         }
         if (left > 0 && (s = launch_steps(c, left)) != GQMAP_OK) return s;
         GQ_HIP(hipGetLastError());
+        // one round trip: Ctl, the chunk's trace slots (as many as may have
+        // run) and the persistent failure word
+        const int it_first = h0.it + total;
+        GQ_HIP(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+        if ((trace || aepe) && (s = queue_trace(c, it_first, chunk)) != GQMAP_OK) return s;
+        if (c->d_snap)
+            GQ_HIP(hipMemcpyAsync(c->h_fail, c->d_bar + BAR_FAIL, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+        Ctl h = *c->h_ctl;
         bool recovered = false;
-        if ((s = persist_recover(c, &recovered)) != GQMAP_OK) return s;
-        Ctl h;
-        if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
-        const int ran = h.it - (h0.it + total);
-        if ((s = fetch_trace(c, h0.it + total, ran, trace ? trace + 3 * total : nullptr,
-                             aepe ? aepe + total : nullptr)) != GQMAP_OK)
-            return s;
+        if (c->d_snap && *c->h_fail != 0) {
+            if ((s = persist_recover(c, &recovered)) != GQMAP_OK) return s;
+            if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+        }
+        const int ran = h.it - it_first;
+        copy_trace(c, it_first, std::min(ran, chunk), trace ? trace + 3 * total : nullptr, aepe ? aepe + total : nullptr);
         total += ran;
         if (h.stop || (ran < chunk && !recovered)) break;
     }
@@ -3648,6 +3682,8 @@ void gqmap_destroy(gqmap_ctx *c)
                     c->d_truth, (void *)c->d_bar, c->d_snap, (void *)c->d_snap_ctl};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
+    for (void *p : {(void *)c->h_ctl, (void *)c->h_ring, (void *)c->h_fail})
+        if (p) (void)hipHostFree(p);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
