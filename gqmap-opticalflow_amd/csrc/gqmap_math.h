@@ -231,6 +231,28 @@ GQ_HD R bicubic_cell4(VP VV, uint32_t o, uint32_t M2, R so, R to)
 
 GQ_HD uint32_t cell_elem(int iy, int ix, int M2) { return (uint32_t)(iy - 1) + GQ_UMUL24(M2, ix - 1); }
 
+// Where the bicubic reads the padded frame: element (r, c) (0-based padded
+// row and column) at p[(r - r0) + ld (c - c0)].  WIN = false: the whole frame
+// in memory (ld = M2, origin 0); WIN = true: a tile's staged copy of the
+// rectangle its samples can reach (the kernel's LDS window).  Same values
+// either way, so the same results.
+template <typename VP, bool WIN = false>
+struct TapView {
+    VP p;
+    uint32_t ld;
+    int r0, c0;
+    GQ_HD uint32_t cell(int iy, int ix) const
+    {
+        if constexpr (WIN) return (uint32_t)(iy - 1 - r0) + GQ_UMUL24(ld, ix - 1 - c0);
+        else return cell_elem(iy, ix, (int)ld);
+    }
+};
+template <typename VP>
+GQ_HD TapView<VP, false> frame_view(VP VV, int M2)
+{
+    return TapView<VP, false>{VV, (uint32_t)M2, 0, 0};
+}
+
 // Elements of a padded-frame (VV) buffer: the (Mo+2) x (No+2) frame, then
 // zeros -- one column and a few elements (VV_TAIL, axis_cell_abs: the taps of
 // cell (Mo, No) reach element (Mo+2) * (No+3)).
@@ -291,24 +313,34 @@ GQ_HD void axis_cell_rel(int j, R x, int n, int &ix, R &fr)
 // 4 x interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV.
 // CLAMP = false: the caller guarantees 1 <= jj + x1 < No and 1 <= ii + x2 < Mo
 // for this sample, where every clamp is the identity -- same result.
-template <bool CLAMP = true, typename VP, typename R>
-GQ_HD R sample4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+template <bool CLAMP = true, typename TV, typename R>
+GQ_HD R sample4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2)
 {
     int ix, iy;
     R so, to;
     axis_cell<CLAMP>(jj, x1, No, ix, so);
     axis_cell<CLAMP>(ii, x2, Mo, iy, to);
-    return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, so, to);
+    return bicubic_cell4<R>(V.p, V.cell(iy, ix), V.ld, so, to);
+}
+template <bool CLAMP = true, typename VP, typename R>
+GQ_HD R sample4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+{
+    return sample4_v<CLAMP>(frame_view(VV, M2), Mo, No, ii, jj, x1, x2);
 }
 // fp64 at absolute 1-based positions X (column), Y (row).
-template <bool CLAMP = true, typename VP>
-GQ_HD double sample4_abs(VP VV, int M2, int Mo, int No, double X, double Y)
+template <bool CLAMP = true, typename TV>
+GQ_HD double sample4_abs_v(const TV &V, int Mo, int No, double X, double Y)
 {
     int ix, iy;
     double so, to;
     axis_cell_abs<CLAMP>(X, No, ix, so);
     axis_cell_abs<CLAMP>(Y, Mo, iy, to);
-    return bicubic_cell4<double>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, so, to);
+    return bicubic_cell4<double>(V.p, V.cell(iy, ix), V.ld, so, to);
+}
+template <bool CLAMP = true, typename VP>
+GQ_HD double sample4_abs(VP VV, int M2, int Mo, int No, double X, double Y)
+{
+    return sample4_abs_v<CLAMP>(frame_view(VV, M2), Mo, No, X, Y);
 }
 // interp2-cubic itself (node_pot's Vq, gqmap_gpu_mixture.m:157-176).
 template <bool CLAMP = true, typename VP, typename R>
@@ -336,8 +368,8 @@ GQ_HD R round_ge1(R y)
 // CLAMP = false: the caller guarantees 1 <= jj + x1 < No - 1/64 (and the
 // same for rows; node_unclamped with CTF_MARGIN), so round(y) lies in [1, MM)
 // and no clamp or cap acts -- the same values.
-template <bool CLAMP = true, typename VP, typename R>
-GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+template <bool CLAMP = true, typename TV, typename R>
+GQ_HD R sample_ctf4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2)
 {
     const R y = (((R)ii + x2) - R(1)) * R(64) + R(1), x = (((R)jj + x1) - R(1)) * R(64) + R(1);
     if constexpr (CLAMP) {
@@ -347,13 +379,18 @@ GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
         int ix = (int)Xq, iy = (int)Yq;  // Xq in [1, No]: truncation == floor
         ix = ix > No - 1 ? No - 1 : ix;
         iy = iy > Mo - 1 ? Mo - 1 : iy;
-        return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, Xq - (R)ix, Yq - (R)iy);
+        return bicubic_cell4<R>(V.p, V.cell(iy, ix), V.ld, Xq - (R)ix, Yq - (R)iy);
     } else {
         const R ry = trunc(y + R(0.5)), rx = trunc(x + R(0.5));  // y, x >= 1: round_ge1
         const R Yq = (ry - R(1)) * R(0.015625) + R(1), Xq = (rx - R(1)) * R(0.015625) + R(1);
         const int ix = (int)Xq, iy = (int)Yq;
-        return bicubic_cell4<R>(VV, cell_elem(iy, ix, M2), (uint32_t)M2, GQ_FRACT(Xq), GQ_FRACT(Yq));
+        return bicubic_cell4<R>(V.p, V.cell(iy, ix), V.ld, GQ_FRACT(Xq), GQ_FRACT(Yq));
     }
+}
+template <bool CLAMP = true, typename VP, typename R>
+GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
+{
+    return sample_ctf4_v<CLAMP>(frame_view(VV, M2), Mo, No, ii, jj, x1, x2);
 }
 
 // ---------------------------------------------------------------------------
@@ -684,8 +721,10 @@ GQ_HD NodeCoef<R> node_coef(R o1, R o2, R p)
 // ENG: 0 single-scale mixture, 1 super (4x4 blocks), 2 coarse-to-fine level.
 // CLAMP = false (ENG 0): the caller has checked that no sample of this node
 // is clamped (node_unclamped), so the clamps are skipped -- same results.
-template <int ENG, bool CLAMP = true, typename R, typename TP, typename VP, typename IP>
-GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, int Mo, int No,
+// V: where the taps are read (TapView: the frame, or the single-pixel
+// engines' staged window).
+template <int ENG, bool CLAMP = true, typename R, typename TP, typename TV, typename IP>
+GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, const TV &V, IP I1, int Mo, int No,
                         R eps, const NodeCoef<R> &c, R u1, R u2, int m, int n)
 {
     Sums<R> S;
@@ -699,7 +738,7 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
             for (int k = k0; k < K2; k += dk) {
                 const R X = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], U1));
                 const R Y = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], U2));
-                const R d = fma(sample4_abs<CLAMP>(VV, M2, Mo, No, X, Y), R(-0.25), I);
+                const R d = fma(sample4_abs_v<CLAMP>(V, Mo, No, X, Y), R(-0.25), I);
                 S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
             }
         } else {
@@ -709,8 +748,8 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
             for (int k = k0; k < K2; k += dk) {
                 const R x1 = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], u1));
                 const R x2 = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], u2));
-                const R v4 = ENG == 2 ? sample_ctf4<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2)
-                                      : sample4<CLAMP>(VV, M2, Mo, No, m + 1, n + 1, x1, x2);
+                const R v4 = ENG == 2 ? sample_ctf4_v<CLAMP>(V, Mo, No, m + 1, n + 1, x1, x2)
+                                      : sample4_v<CLAMP>(V, Mo, No, m + 1, n + 1, x1, x2);
                 const R d = fma(v4, R(-0.25), I);
                 S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
             }
@@ -724,7 +763,7 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, VP VV, IP I1, int M2, in
         for (int k = k0; k < K2; k += dk) {
             const R x1 = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], u1));
             const R x2 = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], u2));
-            S.add(tab, k, super_block_sum<R>(VV, M2, Mo, No, i0, j0, x1, x2, eps, I));
+            S.add(tab, k, super_block_sum<R>(V.p, (int)V.ld, Mo, No, i0, j0, x1, x2, eps, I));
         }
     }
     return S;
@@ -745,6 +784,37 @@ GQ_HD bool node_unclamped(const NodeCoef<R> &c, R u1, R u2, int m, int n, int Mo
     return u1 - rx >= R(-n) && u1 + rx < R(No - 1 - n) && u2 - ry >= R(-m) && u2 + ry < R(Mo - 1 - m);
 }
 
+// The padded-frame rectangle (0-based rows e[0]..e[1], columns e[2]..e[3])
+// that holds every tap of the quadrature samples of node (m, n) (0-based;
+// n the global column) with mean (u1, u2), sigma (o1, o2) and correlation p:
+// the sample bound of node_unclamped, |x - u| <= (|a| + |b|) xmax, where
+// |ax| + |bx| = sqrt2 o1 (s + |t|) = sqrt2 o1 max(sqrt(1+p), sqrt(1-p)) =
+// sqrt2 o1 sqrt(1 + |p|) (node_coef; written this way so a kernel that also
+// runs node_coef does not keep its values live), plus a margin over the
+// position rounding and the ctf 1/64 grid (extra), clamped to the frame as
+// the samples are; then the cells' 4 x 4 taps (row / column ix - 1 .. ix + 2;
+// a cell at the last row reads one element past the padded column, which the
+// frame's linear layout holds: the next column's first, at weight +-0).  NaN
+// positions clamp to cell 1 here as in sample(), so they stay inside.
+template <typename R>
+GQ_HD void tap_rect(R o1, R o2, R p, R u1, R u2, int m, int n, int Mo, int No, double xmax, double extra,
+                    int e[4])
+{
+    const double margin = (sizeof(R) == 8 ? 1e-6 : 1e-2) + extra;
+    const double g = GQ_M_SQRT2 * sqrt(1.0 + fabs((double)p)) * xmax * (1.0 + 1e-12);
+    const double rx = g * fabs((double)o1) + margin, ry = g * fabs((double)o2) + margin;
+    const double X = (double)(n + 1) + (double)u1, Y = (double)(m + 1) + (double)u2;
+    const double xlo = fmin(fmax(X - rx, 1.0), (double)No), xhi = fmin(fmax(X + rx, 1.0), (double)No);
+    const double ylo = fmin(fmax(Y - ry, 1.0), (double)Mo), yhi = fmin(fmax(Y + ry, 1.0), (double)Mo);
+    // positions >= 1: truncation == floor; a position at the last pixel may
+    // take cell n - 1 (interp2's cap: the ctf lookup) or n (sample())
+    const int iylo = (int)ylo, ixlo = (int)xlo;
+    e[0] = (iylo < Mo - 1 ? iylo : Mo - 1) - 1;
+    e[1] = (int)yhi + 2;
+    e[2] = (ixlo < No - 1 ? ixlo : No - 1) - 1;
+    e[3] = (int)xhi + 2;
+}
+
 template <typename R>
 GQ_HD Grad<R> node_epi(const Sums<R> &S, const NodeCoef<R> &c, R lamd, bool guard, R T, R a, R o1,
                        R o2, R p, bool raw_energy = false)
@@ -756,7 +826,7 @@ GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R 
                         bool guard, R T, R a, R u1, R u2, R o1, R o2, R p, int m, int n)
 {
     const NodeCoef<R> c = node_coef(o1, o2, p);
-    return node_epi(node_sums<ENG>(tab, 0, K2, 1, VV, I1, M2, Mo, No, eps, c, u1, u2, m, n), c,
+    return node_epi(node_sums<ENG>(tab, 0, K2, 1, frame_view(VV, M2), I1, Mo, No, eps, c, u1, u2, m, n), c,
                     lamd, guard, T, a, o1, o2, p, ENG == 2);
 }
 
