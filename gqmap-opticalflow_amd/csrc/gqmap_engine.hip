@@ -580,7 +580,8 @@ constexpr int win_elems()
     if (!GQ_TAP_LDS || ENG == 1 || Q == 64) return 0;
     constexpr int wgs = Q <= 1 ? (sizeof(R) == 8 ? 3 : 4) : 2;  // workgroups per CU (VGPR-limited)
     constexpr int rest = (int)sizeof(TileLds<R, VT, tile_pix(Q), (Q > 1 && GQ_TAB_LDS), Q == 0, 0>);
-    const int e = ((163840 / wgs - rest - 1024) / (int)sizeof(VT)) & ~63;  // 1 KiB slack for the allocation granule
+    // 4 KiB per workgroup left for the LDS allocation granule
+    const int e = ((163840 / wgs - rest - 4096) / (int)sizeof(VT)) & ~63;
     return e < GQ_TAP_WIN_MAX ? e : GQ_TAP_WIN_MAX;
 }
 template <typename R, typename VT, int ENG, int Q>
