@@ -31,7 +31,6 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
-#include <climits>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -502,14 +501,10 @@ __device__ void fin_apply(const FinParams &F, const double *tot)
 // 2-wave (<= 256 VGPR) schedule.  GQ_MIN_WAVES / GQ_SUPER_WAVES: experiments.
 // smallest lanes-per-node split whose edge jobs prefetch the next job's
 // operands / run fully unrolled (experiments: GQ_PREFETCH_MIN_Q, GQ_UNROLL_MIN_Q)
-template <typename R>
 constexpr int min_waves(int eng, int q)
 {
-    // Q <= 1 single-pixel engines with staged taps: the VGPR count of the
-    // workgroups the window was sized for (win_elems: 3 at fp64, 4 at fp32)
     return GQ_MIN_WAVES > 1 ? GQ_MIN_WAVES
          : eng == 1        ? GQ_SUPER_WAVES
-         : (q <= 1 && GQ_TAP_LDS && GQ_TAP_FORCE_WAVES) ? (sizeof(R) == 8 ? 3 : 4)
          : (q >= 2 && q <= 8) ? GQ_MIDQ_WAVES : 1;
 }
 
@@ -554,7 +549,7 @@ constexpr int arith_q(int q) { return q == 0 ? 1 : q; }  // lanes per node of th
 // LDS of one tile: in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n);
 // in_left: from (m,n-1); red: per-wave partial sums.  Declared by the kernels
 // (one copy whatever the number of iter_tile instantiations).
-template <typename R, typename VT, int TPIX, bool TAB, bool RS, int WIN>
+template <typename R, int TPIX, bool TAB, bool RS>
 struct TileLds {
     R in_up[2][2][TPIX];
     R in_left[2][2][TPIX];
@@ -564,28 +559,9 @@ struct TileLds {
     R tab[TAB ? NTAB * TS : 1];
     // role split: the node phase's gradient (du1, du2, do1, do2, dp, E, da)
     R nd[RS ? 7 : 1][RS ? TPIX : 1];
-    // staged taps (single-pixel engines): the rectangle of the padded frame
-    // the tile's quadrature samples can reach, and the waves' extents of it
-    VT win[WIN > 0 ? WIN : 1];
-    int ext[4][4];
 };
-// Elements of the staged-tap window: what the workgroups that share a CU
-// (the VGPR-limited count: 3 at Q = 1 fp64, 4 at Q = 1 fp32, 2 at Q >= 2)
-// leave of its 160 KiB next to the rest of TileLds.  Not the super engine
-// (its 4x4 blocks read 7x7 windows per pixel block from the frame) and not
-// Q = 64 (k_iter_wn).  GQ_TAP_LDS = 0: every tap from the frame.
-template <typename R, typename VT, int ENG, int Q>
-constexpr int win_elems()
-{
-    if (!GQ_TAP_LDS || ENG == 1 || Q == 64) return 0;
-    constexpr int wgs = Q <= 1 ? (sizeof(R) == 8 ? 3 : 4) : 2;  // workgroups per CU (VGPR-limited)
-    constexpr int rest = (int)sizeof(TileLds<R, VT, tile_pix(Q), (Q > 1 && GQ_TAB_LDS), Q == 0, 0>);
-    // 4 KiB per workgroup left for the LDS allocation granule
-    const int e = ((163840 / wgs - rest - 4096) / (int)sizeof(VT)) & ~63;
-    return e < GQ_TAP_WIN_MAX ? e : GQ_TAP_WIN_MAX;
-}
-template <typename R, typename VT, int ENG, int Q>
-using TileLdsQ = TileLds<R, VT, tile_pix(Q), (Q > 1 && GQ_TAB_LDS), Q == 0, win_elems<R, VT, ENG, Q>()>;
+template <typename R, int Q>
+using TileLdsQ = TileLds<R, tile_pix(Q), (Q > 1 && GQ_TAB_LDS), Q == 0>;
 
 #if GQ_TIMELINE
 // debug builds: per-block stamps (s_memrealtime, 100 MHz) of k_iter
@@ -789,15 +765,6 @@ __device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, 
     if (tid == 0) ctl->arrive = 0;
 }
 
-// The rectangle of the padded frame node (m, n)'s taps lie in (gqmap_math.h
-// tap_rect; n the global column).
-template <int ENG, typename R, typename VT>
-__device__ __forceinline__ void tap_extent(const IterParams<R, VT> &P, R sg_u, R sg_v, R pn, R u1, R u2, int m, int n,
-                                           int e[4])
-{
-    tap_rect(sg_u, sg_v, pn, u1, u2, m, n, P.Mo, P.No, (double)P.gh_xmax, ENG == 2 ? CTF_MARGIN : 0.0, e);
-}
-
 // One tile of one iteration (absolute iteration `it`, reading state buffer
 // `parity`): node and edge gradients, neighbour scatter, clamped ascent into
 // the other buffer, and the tile's exact partial sums into partial row part_r.
@@ -805,7 +772,7 @@ __device__ __forceinline__ void tap_extent(const IterParams<R, VT> &P, R sg_u, R
 // its own copy).  tab_ready: the LDS table is already loaded (persistent).
 template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
-                                          int part_r, TileLdsQ<R, VT, ENG, Q> &lds, int l0, int l1, double Tcur,
+                                          int part_r, TileLdsQ<R, Q> &lds, int l0, int l1, double Tcur,
                                           bool tab_ready)
 {
     constexpr bool RS = Q == 0;                       // role split (node / edge waves)
@@ -813,7 +780,6 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     constexpr int TPIX = tile_pix(Q);                 // nodes per tile
     constexpr int TM = tile_rows(Q), TN = TPIX / TM;  // tile rows x columns
     static_assert(TM * TN == TPIX, "tile");
-    constexpr int WINE = win_elems<R, VT, ENG, Q>();  // staged-tap window (elements; 0: none)
     Ctl *ctl = P.ctl;
     const R *__restrict__ src = parity ? P.st1 : P.st0;
     R *__restrict__ dst = parity ? P.st0 : P.st1;
@@ -872,69 +838,6 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         const R sg_u = valid ? ld_state<COH>(src + i + MNL * 2) : R(0);
         const R sg_v = valid ? ld_state<COH>(src + i + MNL * 3) : R(0);
         const R pn = valid ? ld_state<COH>(src + i + MNL * 4) : R(0);
-        // Staged taps: the rectangle of the padded frame this tile's samples
-        // of component l can reach, copied into LDS once (coalesced column
-        // runs) instead of gathered from L1/L2 per tap; a rectangle larger
-        // than the window keeps the frame.  Same values, same results.
-        bool staged = false;
-        TapView<const VT *, true> wv{lds.win, 0u, 0, 0};
-        if constexpr (WINE > 0) {
-            int e[4] = {INT_MAX, INT_MIN, INT_MAX, INT_MIN};
-            if (inner && do_node) tap_extent<ENG>(P, sg_u, sg_v, pn, mu_u, mu_v, m, n + P.n_off, e);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                e[0] = min(e[0], __shfl_xor(e[0], o, 64));
-                e[1] = max(e[1], __shfl_xor(e[1], o, 64));
-                e[2] = min(e[2], __shfl_xor(e[2], o, 64));
-                e[3] = max(e[3], __shfl_xor(e[3], o, 64));
-            }
-            if (lane == 0)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) lds.ext[wave][q] = e[q];
-            __syncthreads();
-            int r0 = lds.ext[0][0], r1 = lds.ext[0][1], c0 = lds.ext[0][2], c1 = lds.ext[0][3];
-#pragma unroll
-            for (int w = 1; w < BLOCK / 64; ++w) {
-                r0 = min(r0, lds.ext[w][0]); r1 = max(r1, lds.ext[w][1]);
-                c0 = min(c0, lds.ext[w][2]); c1 = max(c1, lds.ext[w][3]);
-            }
-            // workgroup-uniform: scalar registers
-            r0 = __builtin_amdgcn_readfirstlane(r0); r1 = __builtin_amdgcn_readfirstlane(r1);
-            c0 = __builtin_amdgcn_readfirstlane(c0); c1 = __builtin_amdgcn_readfirstlane(c1);
-            const int H = r1 - r0 + 1, Wc = c1 - c0 + 1;
-            // column stride = 16 mod 32 past 16 rows: the lanes of a wave that
-            // sample one column over read 16 banks over
-            const int ld = H <= 16 ? H : ((H - 16 + 31) & ~31) + 16;
-            staged = r1 >= r0 && ld * Wc <= WINE && GQ_TAP_DEBUG != 1;
-            if (staged) {
-                // element x of the column-major H x Wc rectangle: thread tid
-                // takes x = tid + k BLOCK; 8 loads in flight before the stores
-                const int n_el = H * Wc;
-                int rr = tid % H, cc = tid / H;
-                const int sr = BLOCK % H, sc = BLOCK / H;
-                constexpr int SU = 8;
-                for (int x0 = tid; x0 < n_el; x0 += SU * BLOCK) {
-                    VT v[SU];
-                    int d[SU];
-#pragma unroll
-                    for (int k = 0; k < SU; ++k) {
-                        d[k] = -1;
-                        if (x0 + k * BLOCK < n_el) {
-                            v[k] = P.VV[(uint32_t)(r0 + rr) + (uint32_t)P.M2 * (uint32_t)(c0 + cc)];
-                            d[k] = rr + ld * cc;
-                        }
-                        rr += sr;
-                        cc += sc;
-                        if (rr >= H) { rr -= H; ++cc; }
-                    }
-#pragma unroll
-                    for (int k = 0; k < SU; ++k)
-                        if (d[k] >= 0) lds.win[d[k]] = v[k];
-                }
-                wv = TapView<const VT *, true>{lds.win, (uint32_t)ld, r0, c0};
-            }
-            __syncthreads();  // the window (and lds.ext: read by every thread before the next component)
-        }
         Grad<R> nd{};
         R sum_mu0 = 0, sum_mu1 = 0, sum_sg0 = 0, sum_sg1 = 0;  // sum over dir of du1 / do1
         R eE = 0, eda = 0;                                     // sum over the 4 edges
@@ -957,17 +860,10 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                                                                      P.gh_xmax, R(ENG == 2 ? CTF_MARGIN : 0.0)));
         if (inner) {
             const auto fv = frame_view(P.VV, P.M2);
-            Sums<R> S;
-            if (WINE > 0 && staged && GQ_TAP_DEBUG != 2)
-                S = fast ? node_sums<ENG, false>(tab, kj, K2, QA, wv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v, m,
-                                                 n + P.n_off)
-                         : node_sums<ENG, true>(tab, kj, K2, QA, wv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v, m,
-                                                n + P.n_off);
-            else
-                S = fast ? node_sums<ENG, false>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v, m,
-                                                 n + P.n_off)
-                         : node_sums<ENG, true>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v, m,
-                                                n + P.n_off);
+            Sums<R> S = fast ? node_sums<ENG, false>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v,
+                                                     m, n + P.n_off)
+                             : node_sums<ENG, true>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v,
+                                                    m, n + P.n_off);
             if (QA > 1) S = lane_combine<QA>(S);
             nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, sg_u, sg_v, pn, ENG == 2);
             if constexpr (RS) {  // to the edge lane of the same node
@@ -1095,7 +991,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 
 
 template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(BLOCK, min_waves<R>(ENG, Q)) void k_iter(IterParams<R, VT> P)
+__global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
 {
     Ctl *ctl = P.ctl;
     if (ctl->stop) return;
@@ -1120,7 +1016,7 @@ __global__ __launch_bounds__(BLOCK, min_waves<R>(ENG, Q)) void k_iter(IterParams
     // XCD (see tile_of_block): alternate the phase order among them.  Not
     // for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
     const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
-    __shared__ TileLdsQ<R, VT, ENG, Q> lds;
+    __shared__ TileLdsQ<R, Q> lds;
     const int part_r = P.part_off + b;
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
@@ -1479,7 +1375,7 @@ __device__ void pfin_reduce(const FinParams &F, int row0, int rows, double *tot,
 }
 
 template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(Q == 64 ? WN_THREADS : BLOCK, Q == 64 ? 1 : min_waves<R>(ENG, Q))
+__global__ __launch_bounds__(Q == 64 ? WN_THREADS : BLOCK, Q == 64 ? 1 : min_waves(ENG, Q))
 void k_iter_persist(IterParams<R, VT> P, int n_iter)
 {
     Ctl *ctl = P.ctl;
@@ -1523,7 +1419,7 @@ void k_iter_persist(IterParams<R, VT> P, int n_iter)
             __shared__ WnLds<R> lds_wn;
             wn_tile<R, VT, ENG, true>(P, tile, it, parity, T, part_r, lds_wn, j == 0);
         } else {
-            __shared__ TileLdsQ<R, VT, ENG, Q> lds;
+            __shared__ TileLdsQ<R, Q> lds;
             if (edge_first)
                 iter_tile<R, VT, ENG, Q, true, true>(P, tile, it, parity, part_r, lds, 0, P.L, T, j > 0);
             else

@@ -233,9 +233,10 @@ GQ_HD uint32_t cell_elem(int iy, int ix, int M2) { return (uint32_t)(iy - 1) + G
 
 // Where the bicubic reads the padded frame: element (r, c) (0-based padded
 // row and column) at p[(r - r0) + ld (c - c0)].  WIN = false: the whole frame
-// in memory (ld = M2, origin 0); WIN = true: a tile's staged copy of the
-// rectangle its samples can reach (the kernel's LDS window).  Same values
-// either way, so the same results.
+// in memory (ld = M2, origin 0); WIN = true: a copy of a rectangle of it
+// (round 4 measured a per-tile LDS copy of the rectangle a tile's samples can
+// reach: slower, profiles/r04_tap_lds_ab.txt).  Same values either way, so
+// the same results.
 template <typename VP, bool WIN = false>
 struct TapView {
     VP p;
@@ -782,37 +783,6 @@ GQ_HD bool node_unclamped(const NodeCoef<R> &c, R u1, R u2, int m, int n, int Mo
     const R rx = (fabs(c.ax) + fabs(c.bx)) * xmax + margin, ry = (fabs(c.ay) + fabs(c.by)) * xmax + margin;
     // positions relative to the 1-based pixel (n+1, m+1)
     return u1 - rx >= R(-n) && u1 + rx < R(No - 1 - n) && u2 - ry >= R(-m) && u2 + ry < R(Mo - 1 - m);
-}
-
-// The padded-frame rectangle (0-based rows e[0]..e[1], columns e[2]..e[3])
-// that holds every tap of the quadrature samples of node (m, n) (0-based;
-// n the global column) with mean (u1, u2), sigma (o1, o2) and correlation p:
-// the sample bound of node_unclamped, |x - u| <= (|a| + |b|) xmax, where
-// |ax| + |bx| = sqrt2 o1 (s + |t|) = sqrt2 o1 max(sqrt(1+p), sqrt(1-p)) =
-// sqrt2 o1 sqrt(1 + |p|) (node_coef; written this way so a kernel that also
-// runs node_coef does not keep its values live), plus a margin over the
-// position rounding and the ctf 1/64 grid (extra), clamped to the frame as
-// the samples are; then the cells' 4 x 4 taps (row / column ix - 1 .. ix + 2;
-// a cell at the last row reads one element past the padded column, which the
-// frame's linear layout holds: the next column's first, at weight +-0).  NaN
-// positions clamp to cell 1 here as in sample(), so they stay inside.
-template <typename R>
-GQ_HD void tap_rect(R o1, R o2, R p, R u1, R u2, int m, int n, int Mo, int No, double xmax, double extra,
-                    int e[4])
-{
-    const double margin = (sizeof(R) == 8 ? 1e-6 : 1e-2) + extra;
-    const double g = GQ_M_SQRT2 * sqrt(1.0 + fabs((double)p)) * xmax * (1.0 + 1e-12);
-    const double rx = g * fabs((double)o1) + margin, ry = g * fabs((double)o2) + margin;
-    const double X = (double)(n + 1) + (double)u1, Y = (double)(m + 1) + (double)u2;
-    const double xlo = fmin(fmax(X - rx, 1.0), (double)No), xhi = fmin(fmax(X + rx, 1.0), (double)No);
-    const double ylo = fmin(fmax(Y - ry, 1.0), (double)Mo), yhi = fmin(fmax(Y + ry, 1.0), (double)Mo);
-    // positions >= 1: truncation == floor; a position at the last pixel may
-    // take cell n - 1 (interp2's cap: the ctf lookup) or n (sample())
-    const int iylo = (int)ylo, ixlo = (int)xlo;
-    e[0] = (iylo < Mo - 1 ? iylo : Mo - 1) - 1;
-    e[1] = (int)yhi + 2;
-    e[2] = (ixlo < No - 1 ? ixlo : No - 1) - 1;
-    e[3] = (int)xhi + 2;
 }
 
 template <typename R>

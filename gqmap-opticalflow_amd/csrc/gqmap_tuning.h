@@ -67,23 +67,3 @@
 #ifndef GQ_TIMELINE
 #define GQ_TIMELINE 0
 #endif
-// Single-pixel engines: each tile copies the padded-frame rectangle its
-// quadrature samples can reach into LDS and reads its taps there
-// (win_elems in gqmap_engine.hip); 0: every tap gathered from the frame
-#ifndef GQ_TAP_LDS
-#define GQ_TAP_LDS 0
-#endif
-// ... and bound the Q <= 1 kernels' registers to the workgroups per CU the
-// window was sized for
-#ifndef GQ_TAP_FORCE_WAVES
-#define GQ_TAP_FORCE_WAVES 1
-#endif
-// A/B builds only: 1 = extents and barriers but never stage, 2 = stage but
-// read the taps from the frame
-#ifndef GQ_TAP_DEBUG
-#define GQ_TAP_DEBUG 0
-#endif
-// A/B builds only: cap on the staged-tap window (elements)
-#ifndef GQ_TAP_WIN_MAX
-#define GQ_TAP_WIN_MAX (1 << 30)
-#endif

@@ -13,7 +13,6 @@
 //
 // It is also the CPU baseline: the same algorithm as the GPU kernel, OpenMP
 // over columns.
-#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -45,29 +44,11 @@ namespace {
 constexpr int NFIX = 4;
 constexpr int LMAX = 8;  // GQMAP_LMAX
 
-// Window check (tests): every tap a node's samples read must lie inside the
-// node's tap_rect -- the rectangle the kernel stages into LDS for its tile.
-// A view that reads the frame and counts the taps outside the rectangle.
-std::atomic<int> g_window_check{0};
-std::atomic<long long> g_window_violations{0};
-template <typename VP>
-struct CheckedView {
-    VP p;
-    uint32_t ld;
-    int e[4];
-    uint32_t cell(int iy, int ix) const
-    {
-        if (iy - 1 < e[0] || iy + 2 > e[1] || ix - 1 < e[2] || ix + 2 > e[3]) g_window_violations++;
-        return cell_elem(iy, ix, (int)ld);
-    }
-};
-
 template <typename R>
 struct Work {
     const orc_params *P;
     int M, N, L, K2, Mo, No, M2;
     int64_t MN, MNL;
-    double xmax;  // max |Gauss-Hermite node| as the kernel holds it (R)
     std::vector<R> tab, VV, I1;
     std::vector<R> st, nst;                  // 9 planes of MNL
     std::vector<Grad<R>> node, edge;         // node [MNL], edge [MNL*4] (e = dir + 2*uv)
@@ -124,9 +105,6 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
             tabd[tab_at(T_WX, k)] = ww * (xi * xj);
         }
     w.tab.assign(tabd.begin(), tabd.end());
-    w.xmax = 0;
-    for (int k = 0; k < w.K2; ++k) w.xmax = std::max(w.xmax, std::fabs(tabd[tab_at(T_XI, k)]));
-    w.xmax = (double)R(w.xmax);
     const size_t nvv = (size_t)(w.Mo + 2) * (w.No + 2), ni = (size_t)w.Mo * w.No;
     w.VV.assign(VV, VV + nvv);
     w.VV.resize(vv_elems(w.Mo, w.No), R(0));  // zero tail (axis_cell_abs)
@@ -165,14 +143,6 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                     if (inner) {
                         const NodeCoef<R> c = node_coef(st[i + 2 * MNL], st[i + 3 * MNL], st[i + 4 * MNL]);
                         const Sums<R> Sn = split_sums(Q, [&](int k0, int dk) {
-                            if (g_window_check) {  // every tap inside the node's tap_rect (the kernel's window)
-                                CheckedView<const R *> cv{VVp, (uint32_t)w.M2, {0, 0, 0, 0}};
-                                tap_rect(st[i + 2 * MNL], st[i + 3 * MNL], st[i + 4 * MNL], st[i], st[i + MNL], m,
-                                         n + G.n_off, w.Mo, w.No, w.xmax, ENG == 2 ? CTF_MARGIN : 0.0, cv.e);
-                                if (g_window_check == 2) cv.e[2] += 1;  // self-test: one column short
-                                return node_sums<ENG>(tab, k0, w.K2, dk, cv, I1p, w.Mo, w.No, eps, c, st[i],
-                                                      st[i + MNL], m, n + G.n_off);
-                            }
                             return node_sums<ENG>(tab, k0, w.K2, dk, frame_view(VVp, w.M2), I1p, w.Mo, w.No, eps,
                                                   c, st[i], st[i + MNL], m, n + G.n_off);
                         });
@@ -374,14 +344,7 @@ extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)
 // the device's deterministic exp as a plain function (orc_set_map_exp)
 extern "C" double emu_gq_exp(double x) { return gq_exp(x); }
 
-// Window check on (1) / off (0) / with every rectangle one column short (2,
-// the check's self-test); returns the violations counted since the
-// last call and resets them.
-extern "C" long long emu_window_check(int on)
-{
-    g_window_check = on;
-    return g_window_violations.exchange(0);
-}
+
 
 // sample4_abs (fp64) / sample4 (fp32 relative form) at one position, for the
 // cap identity test (tests/test_spec_identities.py): cap = 0 is the kernel's

@@ -279,16 +279,6 @@ def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
     return done, trace[:done].copy(), Tbox[0]
 
 
-def emu_window_check(on: bool) -> int:
-    """Turn the CPU model's window check on / off (every tap of a node's
-    samples inside gqmap_math.h tap_rect, the rectangle the kernel stages
-    into LDS); returns the taps found outside since the last call."""
-    f = lib().emu_window_check
-    f.restype = C.c_longlong
-    f.argtypes = [C.c_int]
-    return int(f(int(on)))
-
-
 def emu_math(fn: int, x) -> np.ndarray:
     """Host evaluation of the shared deterministic math (0 sqrt, 1 log, 2 exp)."""
     x = _f64(np.asarray(x, dtype=np.float64).ravel())
