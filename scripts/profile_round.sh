@@ -11,7 +11,7 @@ mkdir -p $OUT
 run() {  # name, rocprofv3 args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o run --output-format csv -- \
-    python3 bench.py --config $CFG --precision $PREC --steps $STEPS --warmup 5 --no-cpu-baseline \
+    python3 bench.py --config $CFG --precision $PREC --steps $STEPS --warmup 5 --no-cpu-baseline --no-parity \
     > $OUT/$name.log 2>&1
   local rc=$?; echo "$name=$rc"
   return $rc
