@@ -189,7 +189,6 @@ struct IterParams {
     int guard;
     int64_t MNL;
     unsigned *bar;  // k_iter_persist: barrier counters (BAR_WORDS, zero between launches)
-    R *ngrad;       // phase-split iteration: the node gradients (7 planes of MNL) between the two launches
     int spec;       // speculative RCCL tile: run iteration Ctl::it_i / done_i / T_i
 };
 
@@ -771,16 +770,11 @@ __device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, 
 // the other buffer, and the tile's exact partial sums into partial row part_r.
 // Tcur: the temperature of this iteration (Ctl::T; the persistent kernel keeps
 // its own copy).  tab_ready: the LDS table is already loaded (persistent).
-template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false, int PH = 3>
+template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
                                           int part_r, TileLdsQ<R, Q> &lds, int l0, int l1, double Tcur,
                                           bool tab_ready)
 {
-    // PH: 3 the whole iteration; 1 the node phase only (node gradients to
-    // P.ngrad); 2 the rest (the node gradients from P.ngrad) -- the
-    // phase-split iteration, two launches whose kernels each hold fewer
-    // registers than the fused one (more waves per SIMD)
-    R *__restrict__ const ngrad = P.ngrad;
     constexpr bool RS = Q == 0;                       // role split (node / edge waves)
     constexpr int QA = arith_q(Q);                    // lanes per node of the arithmetic
     constexpr int TPIX = tile_pix(Q);                 // nodes per tile
@@ -855,7 +849,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 #pragma unroll
         for (int ph = 0; ph < 2; ++ph) {
         if ((ph == 0) != EDGE_FIRST) {
-        if (do_node && (PH & 1)) {
+        if (do_node) {
         NodeCoef<R> c{};
         if (inner) c = node_coef(sg_u, sg_v, pn);
         // single-scale engine: when no sample of any node of the wave can be
@@ -878,7 +872,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             }
         }
         }
-        } else if (do_edge && (PH & 2)) {
+        } else if (do_edge) {
         // Edge jobs e = dir + 2*uv (rou plane 5+e) for the owned down/right
         // edges, then job 4 on the halo lanes: the edges entering the tile from
         // the row above / the column to the left.  One edge body, streamed into
@@ -943,19 +937,6 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         }
         if (ph == 0) TL_STAMP(1, __builtin_amdgcn_s_memrealtime());
         }
-        if constexpr (PH == 1) {  // node phase only: the node gradient out
-            if (inner && lead) {
-                ngrad[i] = nd.du1; ngrad[i + MNL] = nd.du2; ngrad[i + 2 * MNL] = nd.do1; ngrad[i + 3 * MNL] = nd.do2;
-                ngrad[i + 4 * MNL] = nd.dp; ngrad[i + 5 * MNL] = nd.E; ngrad[i + 6 * MNL] = nd.da;
-            }
-            continue;
-        }
-        if constexpr (PH == 2) {
-            if (inner && lead) {
-                nd.du1 = ngrad[i]; nd.du2 = ngrad[i + MNL]; nd.do1 = ngrad[i + 2 * MNL]; nd.do2 = ngrad[i + 3 * MNL];
-                nd.dp = ngrad[i + 4 * MNL]; nd.E = ngrad[i + 5 * MNL]; nd.da = ngrad[i + 6 * MNL];
-            }
-        }
         __syncthreads();
         TL_STAMP(2, __builtin_amdgcn_s_memrealtime());
         fix128 fda = 0;
@@ -980,7 +961,6 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     }
 
     TL_STAMP(3, __builtin_amdgcn_s_memrealtime());
-    if constexpr (PH == 1) return;
     // block partials: Energy, sum|dmu_u|, sum|dsigma_u|, #nonfinite, dalpha[0..L-1]
     fE = wave_sum_fix(fE);
     fmu = wave_sum_fix(fmu);
@@ -1010,7 +990,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 }
 
 
-template <typename R, typename VT, int ENG, int Q, int PH = 3>
+template <typename R, typename VT, int ENG, int Q>
 __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
 {
     Ctl *ctl = P.ctl;
@@ -1040,15 +1020,12 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     const int part_r = P.part_off + b;
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
-    } else if (edge_first && PH == 3)
-        iter_tile<R, VT, ENG, Q, true, false, PH>(P, tile, P.spec ? ctl->it_i : ctl->it,
-                                                  (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
-                                                  P.spec ? ctl->T_i : ctl->T, false);
+    } else if (edge_first)
+        iter_tile<R, VT, ENG, Q, true>(P, tile, P.spec ? ctl->it_i : ctl->it, (P.spec ? ctl->done_i : ctl->done) & 1,
+                                       part_r, lds, l0, l1, P.spec ? ctl->T_i : ctl->T, false);
     else
-        iter_tile<R, VT, ENG, Q, false, false, PH>(P, tile, P.spec ? ctl->it_i : ctl->it,
-                                                   (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
-                                                   P.spec ? ctl->T_i : ctl->T, false);
-    if constexpr (PH == 1) return;  // node phase only: the second launch finishes the iteration
+        iter_tile<R, VT, ENG, Q, false>(P, tile, P.spec ? ctl->it_i : ctl->it, (P.spec ? ctl->done_i : ctl->done) & 1,
+                                        part_r, lds, l0, l1, P.spec ? ctl->T_i : ctl->T, false);
 #if GQ_TIMELINE
     __syncthreads();
     TL_STAMP(0, tl0);
@@ -1745,8 +1722,6 @@ struct gqmap_ctx {
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
     int split = 1;      // lanes per node of the arithmetic (Q): 1, 2, 4, 8, 16, 64
     int kq = 1;         // kernel shape: split, or 0 = role split (Q = 1 arithmetic, 16 x 8 tiles)
-    bool phase_split = false;  // Q = 1 whole grid: node phase and the rest as two launches (d_ngrad)
-    void *d_ngrad = nullptr;
     int lpar = 1;       // k_iter blocks per tile (components spread over blocks)
     hipGraphExec_t graph = nullptr;
     // graphs of 2^k iterations (k < SUB_GRAPHS) for the part of a run below
@@ -1873,25 +1848,9 @@ void tile_grid(gqmap_ctx *c)
     c->nblocks = c->tiles_m * c->tiles_n * c->lpar;
 }
 
-// The phase-split iteration (GQMAP_PHASE_SPLIT, default on): Q = 1 single-
-// pixel whole grids run the node phase and the rest of the iteration as two
-// launches -- node-only and edge-only kernels need fewer registers than the
-// fused one (more waves per SIMD) for 2 x 7 node-gradient values per node of
-// extra traffic.  Same arithmetic, same bits.
-bool want_phase_split(const gqmap_ctx *c)
-{
-    static const char *e = std::getenv("GQMAP_PHASE_SPLIT");
-    const bool on = e && *e ? *e == '1' : GQ_PHASE_SPLIT != 0;
-    return on && c->kq == 1 && !c->super_ && c->n_tiles == 1;
-}
-
 gqmap_status alloc_grid(gqmap_ctx *c)
 {
     tile_grid(c);
-    c->phase_split = want_phase_split(c);
-    if (c->d_ngrad) (void)hipFree(c->d_ngrad);
-    c->d_ngrad = nullptr;
-    if (c->phase_split) GQ_HIP(hipMalloc(&c->d_ngrad, (size_t)c->MNL * 7 * c->rsz));
     const size_t bytes = (size_t)c->MNL * NPLANES * c->rsz;
     for (int b = 0; b < 2; ++b) {
         if (c->d_st[b]) (void)hipFree(c->d_st[b]);
@@ -1993,7 +1952,6 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     P.bar = c->d_bar;
-    P.ngrad = (R *)c->d_ngrad;
     return P;
 }
 
@@ -2053,17 +2011,6 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
     if (c->lpar > 1 && P.fused && !sg && lpar_xcd) {
         P.lpar_xcd = 1;
         nblocks = 8 * c->lpar * ((c->tiles_m * c->tiles_n + 7) / 8);
-    }
-    if constexpr (Q == 1 && ENG != 1) {
-        if (c->phase_split && !sg && !c->comm) {
-            static const int2 sh1 = kernel_shape(k_iter<R, VT, ENG, 1, 1>), sh2 = kernel_shape(k_iter<R, VT, ENG, 1, 2>);
-            IterParams<R, VT> P1 = P, P2 = P;
-            P1.cu_group = sh1.x;
-            P2.cu_group = sh2.x;
-            k_iter<R, VT, ENG, 1, 1><<<nblocks, BLOCK, 0, c->stream>>>(P1);
-            k_iter<R, VT, ENG, 1, 2><<<nblocks, BLOCK, 0, c->stream>>>(P2);
-            return;
-        }
     }
     k_iter<R, VT, ENG, Q><<<nblocks, BLOCK, 0, c->stream>>>(P);
 }
@@ -3733,7 +3680,7 @@ void gqmap_destroy(gqmap_ctx *c)
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace,
-                    c->d_truth, (void *)c->d_bar, c->d_snap, (void *)c->d_snap_ctl, c->d_ngrad};
+                    c->d_truth, (void *)c->d_bar, c->d_snap, (void *)c->d_snap_ctl};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     for (void *p : {(void *)c->h_ctl, (void *)c->h_ring, (void *)c->h_fail})

@@ -67,8 +67,3 @@
 #ifndef GQ_TIMELINE
 #define GQ_TIMELINE 0
 #endif
-// Q = 1 single-pixel whole grids: the node phase and the rest of the
-// iteration as two launches (GQMAP_PHASE_SPLIT=0/1 overrides at run time)
-#ifndef GQ_PHASE_SPLIT
-#define GQ_PHASE_SPLIT 0
-#endif
