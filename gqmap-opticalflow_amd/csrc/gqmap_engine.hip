@@ -540,17 +540,11 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
 // Q = 0 (kernel shape only): the role split -- Q = 1 arithmetic on 16 x 8
 // tiles, lanes 0-127 (waves 0-1) run the node phase, lanes 128-255 (waves
 // 2-3) the edge phase of the same nodes, side by side (iter_tile).
-// Q = QW12 (kernel shape only): the Q = 1 arithmetic on 16 x 12 tiles of
-// 192 threads (3 waves) -- chosen where it spreads the grid's work more evenly
-// over the CUs than 16 x 16 tiles (tile_grid).
 constexpr int WN_TM = 5;
-constexpr int QW12 = 112;
-constexpr int tile_pix(int q) { return q == 0 ? BLOCK / 2 : q == 64 ? WN_TM : q == QW12 ? 192 : BLOCK / q; }
-constexpr int tile_rows(int q) { return q <= 2 || q == QW12 ? 16 : q <= 8 ? 8 : q == 64 ? WN_TM : 4; }
+constexpr int tile_pix(int q) { return q == 0 ? BLOCK / 2 : q == 64 ? WN_TM : BLOCK / q; }
+constexpr int tile_rows(int q) { return q <= 2 ? 16 : q <= 8 ? 8 : q == 64 ? WN_TM : 4; }
 constexpr int tile_cols(int q) { return q == 64 ? 1 : tile_pix(q) / tile_rows(q); }
-constexpr int arith_q(int q) { return q == 0 || q == QW12 ? 1 : q; }  // lanes per node of the arithmetic
-// threads of a k_iter workgroup
-constexpr int tile_threads(int q) { return q == 0 ? BLOCK : q == 64 ? 64 * WN_TM : tile_pix(q) * arith_q(q); }
+constexpr int arith_q(int q) { return q == 0 ? 1 : q; }  // lanes per node of the arithmetic
 
 // LDS of one tile: in_up[uv][q][pix]: du2/do2 of the edge from (m-1,n);
 // in_left: from (m,n-1); red: per-wave partial sums.  Declared by the kernels
@@ -567,7 +561,7 @@ struct TileLds {
     R nd[RS ? 7 : 1][RS ? TPIX : 1];
 };
 template <typename R, int Q>
-using TileLdsQ = TileLds<R, tile_pix(Q), (arith_q(Q) > 1 && GQ_TAB_LDS), Q == 0>;
+using TileLdsQ = TileLds<R, tile_pix(Q), (Q > 1 && GQ_TAB_LDS), Q == 0>;
 
 #if GQ_TIMELINE
 // debug builds: per-block stamps (s_memrealtime, 100 MHz) of k_iter
@@ -813,7 +807,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     tab_t tab;
     if constexpr (TAB_LDS) {
         if (!tab_ready) {
-            for (int e = threadIdx.x; e < NTAB * K2; e += tile_threads(Q)) lds.tab[e] = P.tab[e];
+            for (int e = threadIdx.x; e < NTAB * K2; e += BLOCK) lds.tab[e] = P.tab[e];
             __syncthreads();
         }
         tab = lds.tab;
@@ -985,10 +979,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     if (tid < NP) {  // NP <= 12: all in wave 0
         fix128 v = 0;
         const int lq = tid - NFIX;  // dalpha of the components this block ran
-        if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1)) {
-#pragma unroll
-            for (int w = 0; w < tile_threads(Q) / 64; ++w) v += red[tid][w];  // exact: any order
-        }
+        if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1))
+            v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
         if (P.fused || P.tile_acc) {
             if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
         } else {
@@ -999,7 +991,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 
 
 template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(tile_threads(Q), min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
+__global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
 {
     Ctl *ctl = P.ctl;
     if (ctl->stop) return;
@@ -1838,31 +1830,6 @@ void strip_geometry(gqmap_ctx *c, int Mo, int No)
     c->MNL = (int64_t)c->M * c->N * c->L;
 }
 
-// CUs of the device the context runs on (256 on MI355X; the host-only
-// geometry export runs without a device)
-int device_cus(int dev)
-{
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    return cus;
-}
-
-// Q = 1 single-pixel engines: 16 x 16 or 16 x 12 tiles, whichever leaves the
-// busiest CU the least work.  A launch of T tiles spreads over the CUs in
-// whole tiles, so the busiest CU runs ceil(T / CUs) of them; its work, in
-// nodes, sets the launch time (profiles/r04_tile_count_sweep.txt: C2 at 768
-// 16 x 16 tiles, 3 per CU, 122 us; 792 tiles, 24 CUs with a fourth, 152 us).
-// C2 388 x 584: 925 tiles of 256 -> 4 x 256 = 1024 nodes; 1225 of 192 ->
-// 5 x 192 = 960.  GQMAP_TILE_SHAPE=16 / 12 forces one.
-int q1_shape(int M, int N, int cus)
-{
-    static const char *e = std::getenv("GQMAP_TILE_SHAPE");
-    if (e && *e) return atoi(e) == 12 ? QW12 : 1;
-    const int64_t t16 = (int64_t)((M + 15) / 16) * ((N + 15) / 16), t12 = (int64_t)((M + 15) / 16) * ((N + 11) / 12);
-    const int64_t w16 = (t16 + cus - 1) / cus * 256, w12 = (t12 + cus - 1) / cus * 192;
-    return w12 < w16 ? QW12 : 1;
-}
-
 // Lanes per node, kernel shape and the tile grid of the local node grid.
 void tile_grid(gqmap_ctx *c)
 {
@@ -1874,7 +1841,6 @@ void tile_grid(gqmap_ctx *c)
         c->split = 1;
         c->kq = 0;
     }
-    if (c->kq == 1 && !c->super_ && c->opt.split == 0) c->kq = q1_shape(c->M, c->N, device_cus(c->device));
     const int tr = tile_rows(c->kq), tc = tile_cols(c->kq);
     c->tiles_m = (c->M + tr - 1) / tr;
     c->tiles_n = (c->N + tc - 1) / tc;
@@ -2011,10 +1977,10 @@ FinParams fin_params(const gqmap_ctx *c)
 // Resident workgroups per CU for a k_iter instantiation, and CUs per XCD:
 // the tile grouping of k_iter (speed only, never results).
 template <typename K>
-int2 kernel_shape(K kern, int threads = BLOCK)
+int2 kernel_shape(K kern)
 {
     int per_cu = 1, dev = 0, cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0) != hipSuccess) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BLOCK, 0) != hipSuccess) per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     return make_int2(std::max(1, per_cu), std::max(8, cus));
@@ -2034,7 +2000,7 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
         nblocks = (sg->n[0] + sg->n[1]) * c->lpar;
         if (nblocks == 0) return;
     }
-    static const int2 shape = kernel_shape(k_iter<R, VT, ENG, Q>, tile_threads(Q));
+    static const int2 shape = kernel_shape(k_iter<R, VT, ENG, Q>);
     if (!getenv("GQMAP_NO_CU_GROUP")) {
         P.cu_group = shape.x;
         P.cu_slots = std::max(1, shape.y / 8);
@@ -2046,7 +2012,7 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
         P.lpar_xcd = 1;
         nblocks = 8 * c->lpar * ((c->tiles_m * c->tiles_n + 7) / 8);
     }
-    k_iter<R, VT, ENG, Q><<<nblocks, tile_threads(Q), 0, c->stream>>>(P);
+    k_iter<R, VT, ENG, Q><<<nblocks, BLOCK, 0, c->stream>>>(P);
 }
 
 // Q = 64 (one wave per node, k_iter_wn): tiles of 4 x 1 nodes
@@ -2076,7 +2042,6 @@ void launch_iter_q(gqmap_ctx *c, const TileSegs *sg)
     if constexpr (ENG != 1) {
         if (c->kq == 64) return launch_k_iter_wn<R, VT, ENG>(c, sg);
         if (c->kq == 0) return launch_k_iter<R, VT, ENG, 0>(c, sg);
-        if (c->kq == QW12) return launch_k_iter<R, VT, ENG, QW12>(c, sg);
     }
     if (c->split == 16)
         launch_k_iter<R, VT, ENG, 16>(c, sg);

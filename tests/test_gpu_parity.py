@@ -471,25 +471,3 @@ def test_super_bit_exact_on_preprocessed_frames(precision):
         done, tr = eng.run(20)
         g = eng.get_state()
     _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
-
-
-def test_tile_shape_16x12_bit_exact_with_16x16():
-    # The C2 pair runs 16 x 12 tiles (192 threads) by default; the Q = 1
-    # arithmetic is per node, so 16 x 16 tiles (forced split=1) give the same
-    # bits: full frame, 30 iterations from the reference init, plus a crop
-    import ctypes as C
-    from gqmap_opticalflow_amd import Engine, _lib
-    from tests import _fullsize as F
-    lib = _lib.load()
-    lib.gqmap_debug_kernel_shape.argtypes = [C.c_void_p]
-    I1, I2, _, _, o, st = F.case("c2", "ref")
-    out = []
-    for split in (0, 1):
-        with Engine(dict(o, split=split), I1, I2, "mixture", "fp64") as eng:
-            assert lib.gqmap_debug_kernel_shape(eng.ctx) == (112 if split == 0 else 1)
-            eng.set_state(st)
-            done, tr = eng.run(30)
-            out.append((tr, eng.get_state()))
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    for k in G.STATE_KEYS:
-        np.testing.assert_array_equal(getattr(out[0][1], k), getattr(out[1][1], k), err_msg=k)

@@ -212,7 +212,7 @@ def test_rccl_iteration_ticket_counts_launched_blocks(engine):
     f = lib.gqmap_debug_strip_launch
     f.restype = C.c_int
     f.argtypes = [C.POINTER(_lib.GqmapOptions), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
-    tile_cols = {64: 1, 16: 4, 8: 4, 4: 8, 2: 8, 1: 16, 0: 8, 112: 12}
+    tile_cols = {64: 1, 16: 4, 8: 4, 4: 8, 2: 8, 1: 16, 0: 8}
     sup = engine == "super"
     cases = ([(120, 160, 2, 0), (120, 160, 3, 0), (480, 640, 4, 0), (120, 160, 2, 16)] if sup else
              [(30, 40, 2, 0), (30, 40, 3, 64), (60, 80, 4, 0), (60, 80, 2, 64), (388, 584, 8, 4),
@@ -236,28 +236,3 @@ def test_rccl_iteration_ticket_counts_launched_blocks(engine):
                 hit_wn = True
                 assert it_blocks == nblocks - tm
     assert sup or hit_wn
-
-
-def test_q1_tile_shape_policy():
-    # Q = 1 grids take 16 x 12 tiles where that leaves the busiest CU less
-    # work than 16 x 16 (256 CUs; profiles/r04_tile_count_sweep.txt): the C2
-    # pair yes (1225 tiles of 192 nodes -> 5 x 192 = 960 < 4 x 256), C3's
-    # finest level and a C5 frame no; a forced split keeps 16 x 16
-    import ctypes as C
-    from gqmap_opticalflow_amd import _lib
-    from gqmap_opticalflow_amd.engine import make_options
-    lib = _lib.load()
-    f = lib.gqmap_debug_strip_launch
-    f.restype = C.c_int
-    f.argtypes = [C.POINTER(_lib.GqmapOptions), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]
-
-    def shape(Mo, No, engine="mixture", split=0):
-        o = make_options(dict(K=9, L=1, split=split, minu=-1, maxu=1, minv=-1, maxv=1), engine)
-        out = (C.c_int * 5)()
-        assert f(C.byref(o), Mo, No, 1, 0, out) == 0
-        return list(out)
-
-    nb, _, tm, tn, kq = shape(388, 584)
-    assert (kq, tm, tn, nb) == (112, 25, 49, 1225)
-    assert shape(480, 640, "ctf")[4] == 1 and shape(1920, 2560)[4] == 1
-    assert shape(388, 584, split=1)[4] == 1
