@@ -606,6 +606,7 @@ template <bool COH, typename R>
 __device__ __forceinline__ void st_state(R *p, R v)
 {
     if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if constexpr (GQ_STATE_NT_STORE) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
