@@ -189,6 +189,7 @@ struct IterParams {
     int guard;
     int64_t MNL;
     unsigned *bar;  // k_iter_persist: barrier counters (BAR_WORDS, zero between launches)
+    int nt_state;   // state stores non-temporal (state_nt)
     int spec;       // speculative RCCL tile: run iteration Ctl::it_i / done_i / T_i
 };
 
@@ -602,11 +603,14 @@ __device__ __forceinline__ R ld_state(const R *p)
     if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else return *p;
 }
+// nt: a non-temporal store -- the state of a frame larger than the L2s is
+// streamed once per iteration; kept out of the L2 it does not evict the
+// padded frame's gather lines (C5: fetch bytes -16%, profiles/r04_c5_nt_store.txt)
 template <bool COH, typename R>
-__device__ __forceinline__ void st_state(R *p, R v)
+__device__ __forceinline__ void st_state(R *p, R v, bool nt)
 {
     if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else if constexpr (GQ_STATE_NT_STORE) __builtin_nontemporal_store(v, p);
+    else if (nt) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
@@ -672,8 +676,8 @@ __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__re
     const int64_t MNL = P.MNL, MN = (int64_t)M * P.N;
     auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
     const R nu = cl(mu_u + gmu_u * step, P.minu, P.maxu), nv = cl(mu_v + gmu_v * step, P.minv, P.maxv);
-    st_state<COH, R>(dst + i + MNL * 0, nu);
-    st_state<COH, R>(dst + i + MNL * 1, nv);
+    st_state<COH, R>(dst + i + MNL * 0, nu, P.nt_state);
+    st_state<COH, R>(dst + i + MNL * 1, nv, P.nt_state);
     if constexpr (ENG == 2) {  // AEPE of gqmap_ctf.m:38 against the updated mean
         if (P.truth) {
             const double du = P.truth[m + (int64_t)M * n] - (double)nu;
@@ -684,9 +688,9 @@ __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__re
     // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
     const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
     const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
-    st_state<COH, R>(dst + i + MNL * 2, cl(sg_u + su, P.sig_lo, P.sig_hi));
-    st_state<COH, R>(dst + i + MNL * 3, cl(sg_v + sv, P.sig_lo, P.sig_hi));
-    st_state<COH, R>(dst + i + MNL * 4, cl(pn + nd.dp * step, -P.corr, P.corr));
+    st_state<COH, R>(dst + i + MNL * 2, cl(sg_u + su, P.sig_lo, P.sig_hi), P.nt_state);
+    st_state<COH, R>(dst + i + MNL * 3, cl(sg_v + sv, P.sig_lo, P.sig_hi), P.nt_state);
+    st_state<COH, R>(dst + i + MNL * 4, cl(pn + nd.dp * step, -P.corr, P.corr), P.nt_state);
     // per-node contributions to the global sums (exact fixed point)
     const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
     const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
@@ -920,7 +924,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                 // the edge owns its correlation: clamped ascent right here
                 // (gqmap_gpu_mixture.m:46), nothing else reads drou
                 if (own_edge && inner && lead)
-                    st_state<COH, R>(dst + i + MNL * (5 + e), fmin(fmax(jb.p + g.dp * step, -P.corr), P.corr));
+                    st_state<COH, R>(dst + i + MNL * (5 + e), fmin(fmax(jb.p + g.dp * step, -P.corr), P.corr), P.nt_state);
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
@@ -1165,7 +1169,7 @@ __device__ __forceinline__ void wn_tile(const IterParams<R, VT> &P, int tile, in
             Sums<R> S1 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c1);
             S1 = lane_combine<16>(S1);
             const Grad<R> g1 = edge_epi(S1, c1, P.lams, P.guard != 0, T, a, own_o, o2, p1, ENG == 2);
-            if (gl == 0) st_state<COH, R>(dst + i + MNL * (5 + grp), fmin(fmax(p1 + g1.dp * step, -P.corr), P.corr));
+            if (gl == 0) st_state<COH, R>(dst + i + MNL * (5 + grp), fmin(fmax(p1 + g1.dp * step, -P.corr), P.corr), P.nt_state);
             // round 2: the edge entering from the head node h (its edge grp)
             const EdgeCoef<R> c2 = edge_coef(hu, own_u, ho, own_o, p2);
             Sums<R> S2 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c2);
@@ -1903,6 +1907,18 @@ int iteration_blocks(const gqmap_ctx *c)
 
 FinParams fin_params(const gqmap_ctx *c);
 
+// Non-temporal state stores for a state buffer larger than the XCDs' L2s
+// together (8 x 4 MiB): it is streamed once per iteration and would evict
+// the frame's gather lines (C5 fetch 691 -> 582 MB per launch, time -0.4%);
+// a C2-sized buffer (16 MB) is partly still in L2 when the next iteration
+// reads it (round 3: NT stores on C2 +0.8%).  GQMAP_NT_STATE=0/1 forces.
+bool state_nt(const gqmap_ctx *c)
+{
+    static const char *e = std::getenv("GQMAP_NT_STATE");
+    if (e && *e) return *e == '1';
+    return (size_t)c->MNL * NPLANES * c->rsz > ((size_t)32 << 20);
+}
+
 bool fused_finalize(const gqmap_ctx *c)
 {
     static const bool off = std::getenv("GQMAP_NO_FUSED_FINALIZE") != nullptr;
@@ -1953,6 +1969,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     P.bar = c->d_bar;
+    P.nt_state = state_nt(c) ? 1 : 0;
     return P;
 }
 

@@ -67,8 +67,3 @@
 #ifndef GQ_TIMELINE
 #define GQ_TIMELINE 0
 #endif
-// State stores of the per-iteration kernels as non-temporal (streamed once:
-// kept out of the L2 the frame's gather windows live in)
-#ifndef GQ_STATE_NT_STORE
-#define GQ_STATE_NT_STORE 0
-#endif
