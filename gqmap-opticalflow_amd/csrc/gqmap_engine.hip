@@ -189,7 +189,6 @@ struct IterParams {
     int guard;
     int64_t MNL;
     unsigned *bar;  // k_iter_persist: barrier counters (BAR_WORDS, zero between launches)
-    int nt_state;   // state stores non-temporal (state_nt)
     int spec;       // speculative RCCL tile: run iteration Ctl::it_i / done_i / T_i
 };
 
@@ -603,14 +602,16 @@ __device__ __forceinline__ R ld_state(const R *p)
     if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else return *p;
 }
-// nt: a non-temporal store -- the state of a frame larger than the L2s is
+// NT: a non-temporal store -- the state of a frame larger than the L2s is
 // streamed once per iteration; kept out of the L2 it does not evict the
-// padded frame's gather lines (C5: fetch bytes -16%, profiles/r04_c5_nt_store.txt)
-template <bool COH, typename R>
-__device__ __forceinline__ void st_state(R *p, R v, bool nt)
+// padded frame's gather lines (C5: fetch bytes -16%, profiles/r04_c5_nt_store.txt).
+// A compile-time choice: a run-time one lets the compiler merge the two
+// stores into one plain store.
+template <bool COH, typename R, bool NT = false>
+__device__ __forceinline__ void st_state(R *p, R v)
 {
     if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else if (nt) __builtin_nontemporal_store(v, p);
+    else if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
@@ -666,7 +667,7 @@ __device__ __forceinline__ EdgeJob<R> edge_job(const IterParams<R, VT> &P, const
 // The clamped ascent of one interior node from its assembled gradients
 // (gqmap_gpu_mixture.m:41-45; gqmap_ctf.m:34-35), the updated state into dst
 // and the node's exact contributions to the block sums; returns its dalpha.
-template <int ENG, bool COH, typename R, typename VT>
+template <int ENG, bool COH, bool NT = false, typename R, typename VT>
 __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__restrict__ dst, int64_t i, int m,
                                              int n, R step, R mu_u, R mu_v, R sg_u, R sg_v, R pn, const Grad<R> &nd,
                                              R gmu_u, R gmu_v, R gsg_u, R gsg_v, R eE, R eda, fix128 &fE,
@@ -676,8 +677,8 @@ __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__re
     const int64_t MNL = P.MNL, MN = (int64_t)M * P.N;
     auto cl = [](R x, R lo, R hi) { return fmin(fmax(x, lo), hi); };
     const R nu = cl(mu_u + gmu_u * step, P.minu, P.maxu), nv = cl(mu_v + gmu_v * step, P.minv, P.maxv);
-    st_state<COH, R>(dst + i + MNL * 0, nu, P.nt_state);
-    st_state<COH, R>(dst + i + MNL * 1, nv, P.nt_state);
+    st_state<COH, R, NT>(dst + i + MNL * 0, nu);
+    st_state<COH, R, NT>(dst + i + MNL * 1, nv);
     if constexpr (ENG == 2) {  // AEPE of gqmap_ctf.m:38 against the updated mean
         if (P.truth) {
             const double du = P.truth[m + (int64_t)M * n] - (double)nu;
@@ -688,9 +689,9 @@ __device__ __forceinline__ fix128 node_apply(const IterParams<R, VT> &P, R *__re
     // sigma step: gqmap_ctf.m:34-35 scales it by 0.3 ((dsigma*step)*0.3)
     const R su = ENG == 2 ? (gsg_u * step) * P.sig_step : gsg_u * step;
     const R sv = ENG == 2 ? (gsg_v * step) * P.sig_step : gsg_v * step;
-    st_state<COH, R>(dst + i + MNL * 2, cl(sg_u + su, P.sig_lo, P.sig_hi), P.nt_state);
-    st_state<COH, R>(dst + i + MNL * 3, cl(sg_v + sv, P.sig_lo, P.sig_hi), P.nt_state);
-    st_state<COH, R>(dst + i + MNL * 4, cl(pn + nd.dp * step, -P.corr, P.corr), P.nt_state);
+    st_state<COH, R, NT>(dst + i + MNL * 2, cl(sg_u + su, P.sig_lo, P.sig_hi));
+    st_state<COH, R, NT>(dst + i + MNL * 3, cl(sg_v + sv, P.sig_lo, P.sig_hi));
+    st_state<COH, R, NT>(dst + i + MNL * 4, cl(pn + nd.dp * step, -P.corr, P.corr));
     // per-node contributions to the global sums (exact fixed point)
     const double cE = (double)nd.E + (double)eE, cda = (double)nd.da + (double)eda;
     const double cmu = fabs((double)gmu_u), csg = fabs((double)gsg_u);
@@ -775,7 +776,7 @@ __device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, 
 // the other buffer, and the tile's exact partial sums into partial row part_r.
 // Tcur: the temperature of this iteration (Ctl::T; the persistent kernel keeps
 // its own copy).  tab_ready: the LDS table is already loaded (persistent).
-template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false>
+template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false, bool NT = false>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
                                           int part_r, TileLdsQ<R, Q> &lds, int l0, int l1, double Tcur,
                                           bool tab_ready)
@@ -924,7 +925,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                 // the edge owns its correlation: clamped ascent right here
                 // (gqmap_gpu_mixture.m:46), nothing else reads drou
                 if (own_edge && inner && lead)
-                    st_state<COH, R>(dst + i + MNL * (5 + e), fmin(fmax(jb.p + g.dp * step, -P.corr), P.corr), P.nt_state);
+                    st_state<COH, R, NT>(dst + i + MNL * (5 + e), fmin(fmax(jb.p + g.dp * step, -P.corr), P.corr));
             }
             if (own_edge) {
                 if (uv == 0) { sum_mu0 = sum_mu0 + g.du1; sum_sg0 = sum_sg0 + g.do1; }
@@ -955,7 +956,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             const R gmu_v = ((nd.du2 + sum_mu1) + in_up[1][0][pix]) + in_left[1][0][pix];
             const R gsg_u = ((nd.do1 + sum_sg0) + in_up[0][1][pix]) + in_left[0][1][pix];
             const R gsg_v = ((nd.do2 + sum_sg1) + in_up[1][1][pix]) + in_left[1][1][pix];
-            fda = node_apply<ENG, COH>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u, gsg_v,
+            fda = node_apply<ENG, COH, NT>(P, dst, i, m, n, step, mu_u, mu_v, sg_u, sg_v, pn, nd, gmu_u, gmu_v, gsg_u, gsg_v,
                                   eE, eda, fE, fmu, fsg, fae, nonfinite);
         }
         if (P.L > 1) {  // dalpha(l): only consumed by the alpha update
@@ -995,7 +996,7 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 }
 
 
-template <typename R, typename VT, int ENG, int Q>
+template <typename R, typename VT, int ENG, int Q, bool NT = false>
 __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
 {
     Ctl *ctl = P.ctl;
@@ -1026,11 +1027,13 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
     } else if (edge_first)
-        iter_tile<R, VT, ENG, Q, true>(P, tile, P.spec ? ctl->it_i : ctl->it, (P.spec ? ctl->done_i : ctl->done) & 1,
-                                       part_r, lds, l0, l1, P.spec ? ctl->T_i : ctl->T, false);
+        iter_tile<R, VT, ENG, Q, true, false, NT>(P, tile, P.spec ? ctl->it_i : ctl->it,
+                                                  (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
+                                                  P.spec ? ctl->T_i : ctl->T, false);
     else
-        iter_tile<R, VT, ENG, Q, false>(P, tile, P.spec ? ctl->it_i : ctl->it, (P.spec ? ctl->done_i : ctl->done) & 1,
-                                        part_r, lds, l0, l1, P.spec ? ctl->T_i : ctl->T, false);
+        iter_tile<R, VT, ENG, Q, false, false, NT>(P, tile, P.spec ? ctl->it_i : ctl->it,
+                                                   (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
+                                                   P.spec ? ctl->T_i : ctl->T, false);
 #if GQ_TIMELINE
     __syncthreads();
     TL_STAMP(0, tl0);
@@ -1169,7 +1172,7 @@ __device__ __forceinline__ void wn_tile(const IterParams<R, VT> &P, int tile, in
             Sums<R> S1 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c1);
             S1 = lane_combine<16>(S1);
             const Grad<R> g1 = edge_epi(S1, c1, P.lams, P.guard != 0, T, a, own_o, o2, p1, ENG == 2);
-            if (gl == 0) st_state<COH, R>(dst + i + MNL * (5 + grp), fmin(fmax(p1 + g1.dp * step, -P.corr), P.corr), P.nt_state);
+            if (gl == 0) st_state<COH, R>(dst + i + MNL * (5 + grp), fmin(fmax(p1 + g1.dp * step, -P.corr), P.corr));
             // round 2: the edge entering from the head node h (its edge grp)
             const EdgeCoef<R> c2 = edge_coef(hu, own_u, ho, own_o, p2);
             Sums<R> S2 = edge_sums_dev(tab, gl, K2, 16, P.epsn, c2);
@@ -1969,7 +1972,6 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     P.bar = c->d_bar;
-    P.nt_state = state_nt(c) ? 1 : 0;
     return P;
 }
 
@@ -2029,6 +2031,12 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
     if (c->lpar > 1 && P.fused && !sg && lpar_xcd) {
         P.lpar_xcd = 1;
         nblocks = 8 * c->lpar * ((c->tiles_m * c->tiles_n + 7) / 8);
+    }
+    if constexpr (Q == 1 && ENG != 1) {
+        if (state_nt(c)) {  // frames beyond the L2s: non-temporal state stores
+            k_iter<R, VT, ENG, 1, true><<<nblocks, BLOCK, 0, c->stream>>>(P);
+            return;
+        }
     }
     k_iter<R, VT, ENG, Q><<<nblocks, BLOCK, 0, c->stream>>>(P);
 }

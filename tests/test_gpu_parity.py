@@ -471,3 +471,30 @@ def test_super_bit_exact_on_preprocessed_frames(precision):
         done, tr = eng.run(20)
         g = eng.get_state()
     _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
+
+
+def test_nontemporal_state_stores_same_bits():
+    # state_nt (non-temporal state stores, and own-state loads where built
+    # in) is a cache policy: forced on, a C2 crop gives the same trace and
+    # state as forced off (separate processes: the policy is read once)
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, ".")
+from tests.test_gpu_parity import _reference_init_case, _run_engine
+I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 128, 160, 100, 150, L=1, K=9)
+_, tr, g, _ = _run_engine(o, I1, I2, "mixture", "fp64", st, 60)
+np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigu.ravel(), g.pn.ravel(), g.rou.ravel()]))
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as d:
+        outs = []
+        for v in ("0", "1"):
+            env = dict(os.environ, GQMAP_NT_STATE=v)
+            f = os.path.join(d, f"nt{v}.npy")
+            subprocess.run([sys.executable, "-c", code, f], cwd=root, env=env, check=True, timeout=300)
+            outs.append(np.load(f))
+    np.testing.assert_array_equal(outs[0], outs[1])
