@@ -1723,6 +1723,11 @@ struct gqmap_ctx {
     Ctl *h_ctl = nullptr;
     double *h_ring = nullptr;
     unsigned *h_fail = nullptr;
+    // Ctl::it as the host last saw it (read_ctl / upload_ctl / the end of
+    // gqmap_run_aepe); every launch that may advance Ctl clears ctl_known, so
+    // back-to-back runs skip the round trip that reads the starting iteration
+    int ctl_it = 0;
+    bool ctl_known = false;
     double *d_truth = nullptr;  // gqmap_set_truth: M x N x 2 (ctf engine)
     size_t truth_elems = 0;     // doubles d_truth was allocated for
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
@@ -2094,6 +2099,7 @@ void launch_iter_t(gqmap_ctx *c, const TileSegs *sg)
 // sg: a subset of the tiles (default: all, one launch)
 void launch_iter(gqmap_ctx *c, const TileSegs *sg = nullptr)
 {
+    c->ctl_known = false;
     if (c->fp32) launch_iter_t<float, float>(c, sg);
     else if (c->vv32) launch_iter_t<double, vvs_t>(c, sg);
     else launch_iter_t<double, double>(c, sg);
@@ -2313,6 +2319,7 @@ void unpack_finalize_t(gqmap_ctx *c)
 }
 void unpack_finalize(gqmap_ctx *c)
 {
+    c->ctl_known = false;
     if (c->fp32) unpack_finalize_t<float>(c);
     else unpack_finalize_t<double>(c);
 }
@@ -2489,6 +2496,7 @@ gqmap_status join_spec(gqmap_ctx *c)
 
 gqmap_status launch_step(gqmap_ctx *c)
 {
+    c->ctl_known = false;
     if (c->comm) return rccl_spec(c) ? launch_step_rccl_spec(c) : launch_step_rccl(c);
     launch_iter(c);
     return launch_tail(c);
@@ -2497,6 +2505,7 @@ gqmap_status launch_step(gqmap_ctx *c)
 // n iterations: one persistent launch for small ctf grids, else n steps
 gqmap_status launch_steps(gqmap_ctx *c, int n)
 {
+    c->ctl_known = false;
     if (launch_persist(c, n)) return GQMAP_OK;
     gqmap_status st = GQMAP_OK;
     for (int i = 0; i < n && st == GQMAP_OK; ++i) st = launch_step(c);
@@ -2520,6 +2529,7 @@ gqmap_status persist_recover(gqmap_ctx *c, bool *recovered)
 {
     *recovered = false;
     if (!c->d_snap) return GQMAP_OK;  // no persistent launch has run on this context
+    c->ctl_known = false;
     unsigned f = 0;
     GQ_HIP(hipMemcpyAsync(&f, c->d_bar + BAR_FAIL, sizeof(f), hipMemcpyDeviceToHost, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
@@ -2554,8 +2564,11 @@ gqmap_status upload_ctl(gqmap_ctx *c, int it, double T, const double *w, const d
         h.w[l] = w[l];
         h.alpha[l] = alpha[l];
     }
+    c->ctl_known = false;
     GQ_HIP(hipMemcpyAsync(c->d_ctl, &h, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
+    c->ctl_it = it;
+    c->ctl_known = true;
     return GQMAP_OK;
 }
 
@@ -2564,6 +2577,8 @@ gqmap_status read_ctl(gqmap_ctx *c, Ctl *h)
     GQ_HIP(hipMemcpyAsync(c->h_ctl, c->d_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     *h = *c->h_ctl;
+    c->ctl_it = h->it;
+    c->ctl_known = true;
     return GQMAP_OK;
 }
 
@@ -3145,13 +3160,15 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
     GQ_CHECK(n_iter >= 0, GQMAP_ERR_INVALID_ARG, "n_iter < 0");
     DeviceGuard dg(c->device);
     Ctl h0;
-    gqmap_status s = read_ctl(c, &h0);
-    if (s != GQMAP_OK) return s;
+    gqmap_status s = GQMAP_OK;
+    if (c->ctl_known) h0.it = c->ctl_it;
+    else if ((s = read_ctl(c, &h0)) != GQMAP_OK) return s;
     int total = 0;
     while (total < n_iter) {
         // the device trace ring holds TRACE_CAP iterations: drain it per chunk
         const int chunk = std::min(n_iter - total, TRACE_CAP);
         int left = chunk;
+        c->ctl_known = false;
         static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
         if (!no_graph) {
             // GRAPH_CHUNK-iteration graphs, then the remainder as graphs of
@@ -3187,6 +3204,8 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         const int ran = h.it - it_first;
         copy_trace(c, it_first, std::min(ran, chunk), trace ? trace + 3 * total : nullptr, aepe ? aepe + total : nullptr);
         total += ran;
+        c->ctl_it = h.it;
+        c->ctl_known = true;
         if (h.stop || (ran < chunk && !recovered)) break;
     }
     if (n_done) *n_done = total;
