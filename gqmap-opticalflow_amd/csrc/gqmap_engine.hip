@@ -180,6 +180,9 @@ struct IterParams {
     // past the last tile idle
     int lpar_xcd;
     int cu_group, cu_slots;  // co-resident workgroups per CU, CUs per XCD (tile order only)
+    // whole-grid launch on a frame beyond the L2s: each XCD walks its band of
+    // tile columns row by row (tile_of_block; tile order only)
+    int band_rows;
     FinParams fin;
     R epsn, lamd, lams;
     R minu, maxu, minv, maxv, sig_lo, sig_hi, corr, sig_step;
@@ -511,7 +514,35 @@ constexpr int min_waves(int eng, int q)
 // Tile index of block b: XCD-aware order.  Blocks b and b+8 share an XCD
 // (round-robin dispatch), so each XCD gets a contiguous band of tiles (L2
 // locality of the VV gathers).  Speed only; results never depend on placement.
-__device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
+// Position i of the row-by-row walk over the tiles [s, e) (column-major
+// numbering, TM tile rows): the range covers column cf from row rf down,
+// the full columns cf+1 .. cl-1, and column cl down to row re; row tm holds
+// inner + (tm >= rf) + (tm <= re) of them.  Consecutive tiles of the walk
+// then share the frame lines their samples read -- a band's gather window
+// stays in its XCD's L2 while the state streams through it (down a column,
+// the frame lines are reused only a column of tiles later, ~3.6 MB of state
+// per column on C5 against a 4 MB L2).
+__device__ __forceinline__ int band_row_tile(int i, int s, int e, int TM)
+{
+    const int cf = s / TM, rf = s - cf * TM, cl = (e - 1) / TM, re = (e - 1) - cl * TM;
+    if (cf == cl) return s + i;
+    const int inner = cl - cf - 1;
+    // tiles in rows < tm: tm inner + max(0, tm - rf) + min(tm, re + 1); the
+    // largest tm with that count <= i
+    int lo = 0, hi = TM - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        const int before = mid * inner + max(0, mid - rf) + min(mid, re + 1);
+        if (before <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    const int tm = lo;
+    const int j = i - (tm * inner + max(0, tm - rf) + min(tm, re + 1));
+    const int col = tm >= rf ? cf + j : cf + 1 + j;
+    return col * TM + tm;
+}
+
+__device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S, int band_tm = 0)
 {
     int tile = b >> 3;
     // Within an XCD, local blocks j, j+S, j+2S, ... (S = CUs per XCD) start on
@@ -529,8 +560,10 @@ __device__ __forceinline__ int tile_of_block(int b, int nb, int cu_group, int S)
         }
     }
     const int xcd = b & 7;
-    for (int y = 0; y < xcd; ++y) tile += (nb - y + 7) >> 3;
-    return tile;
+    int s = 0;
+    for (int y = 0; y < xcd; ++y) s += (nb - y + 7) >> 3;
+    if (band_tm > 0) return band_row_tile(tile, s, s + ((nb - xcd + 7) >> 3), band_tm);
+    return s + tile;
 }
 
 // Node rows of a tile with Q lanes per node (256 / Q nodes): 16 x 16, 16 x 8
@@ -1016,7 +1049,7 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     }
     const int l1 = P.lpar > 1 ? l0 + 1 : P.L;
     const bool idle = bt >= nb;  // lpar_xcd padding
-    const int tl = idle ? 0 : tile_of_block(bt, nb, P.cu_group, P.cu_slots);
+    const int tl = idle ? 0 : tile_of_block(bt, nb, P.cu_group, P.cu_slots, P.band_rows ? P.tiles_m : 0);
     const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
     // workgroups that start on one CU are local blocks j, j+S, j+2S of the
     // XCD (see tile_of_block): alternate the phase order among them.  Not
@@ -1927,6 +1960,16 @@ bool state_nt(const gqmap_ctx *c)
     return (size_t)c->MNL * NPLANES * c->rsz > ((size_t)32 << 20);
 }
 
+// Row-by-row tile walk within each XCD's band (tile_of_block) for frames
+// whose padded VV is larger than one XCD's 4 MiB L2.  GQMAP_BAND_ROWS=0/1 forces.
+bool band_rows(const gqmap_ctx *c)
+{
+    static const char *e = std::getenv("GQMAP_BAND_ROWS");
+    if (e && *e) return *e == '1';
+    const size_t vsz = c->fp32 ? sizeof(float) : c->vv32 ? sizeof(vvs_t) : sizeof(double);
+    return vv_elems(c->Mo, c->No) * vsz > ((size_t)4 << 20);
+}
+
 bool fused_finalize(const gqmap_ctx *c)
 {
     static const bool off = std::getenv("GQMAP_NO_FUSED_FINALIZE") != nullptr;
@@ -1976,6 +2019,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     P.spec = c->spec_now ? 1 : 0;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
+    P.band_rows = 0;
     P.bar = c->d_bar;
     return P;
 }
@@ -2037,6 +2081,8 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
         P.lpar_xcd = 1;
         nblocks = 8 * c->lpar * ((c->tiles_m * c->tiles_n + 7) / 8);
     }
+    // (whole grid, one block per tile; lpar_xcd interleaves components instead)
+    if (!sg && !P.lpar_xcd) P.band_rows = band_rows(c) ? 1 : 0;
     if constexpr (Q == 1 && ENG != 1) {
         if (state_nt(c)) {  // frames beyond the L2s: non-temporal state stores
             k_iter<R, VT, ENG, 1, true><<<nblocks, BLOCK, 0, c->stream>>>(P);

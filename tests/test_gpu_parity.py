@@ -498,3 +498,32 @@ np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigu.ravel(), 
             subprocess.run([sys.executable, "-c", code, f], cwd=root, env=env, check=True, timeout=300)
             outs.append(np.load(f))
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_band_row_tile_order_same_bits(precision):
+    # GQMAP_BAND_ROWS (each XCD walks its band of tile columns row by row,
+    # gqmap_engine.hip band_row_tile) is a placement: forced on, a 100 x 150
+    # frame (7 tile rows, 10 tile columns: the bands start and end inside a
+    # tile column) gives the same trace and state as forced off
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, ".")
+from tests.test_gpu_parity import _reference_init_case, _run_engine
+I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 100, 150, 100, 150, L=2, K=9)
+_, tr, g, _ = _run_engine(o, I1, I2, "mixture", sys.argv[2], st, 60)
+np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigu.ravel(), g.pn.ravel(), g.rou.ravel()]))
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as d:
+        outs = []
+        for v in ("0", "1"):
+            env = dict(os.environ, GQMAP_BAND_ROWS=v)
+            f = os.path.join(d, f"band{v}.npy")
+            subprocess.run([sys.executable, "-c", code, f, precision], cwd=root, env=env, check=True, timeout=300)
+            outs.append(np.load(f))
+    np.testing.assert_array_equal(outs[0], outs[1])
