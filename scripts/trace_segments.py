@@ -1,0 +1,22 @@
+"""Per-segment k_iter durations of a rocprofv3 kernel trace of bench.py: the
+launches between two k_init_state dispatches form one segment (warm-up,
+clock-settle chunks, the timed steps, the instrumented replay, ...), so the
+timed window's rocprofv3 mean can be set beside the line's HIP-event mean.
+usage: trace_segments.py <run_kernel_trace.csv>"""
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+segs, cur = [], []
+for r in rows:
+    n = r["Kernel_Name"]
+    if "k_init_state" in n:
+        segs.append(cur)
+        cur = []
+    elif "k_iter" in n:
+        cur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+segs.append(cur)
+print(f"{'segment':>7s} {'launches':>8s} {'mean_us':>8s} {'min_us':>7s} {'max_us':>7s}")
+for i, s in enumerate(segs):
+    if s:
+        print(f"{i:7d} {len(s):8d} {sum(s) / len(s):8.1f} {min(s):7.1f} {max(s):7.1f}")
