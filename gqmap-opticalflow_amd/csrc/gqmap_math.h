@@ -231,27 +231,20 @@ GQ_HD R bicubic_cell4(VP VV, uint32_t o, uint32_t M2, R so, R to)
 
 GQ_HD uint32_t cell_elem(int iy, int ix, int M2) { return (uint32_t)(iy - 1) + GQ_UMUL24(M2, ix - 1); }
 
-// Where the bicubic reads the padded frame: element (r, c) (0-based padded
-// row and column) at p[(r - r0) + ld (c - c0)].  WIN = false: the whole frame
-// in memory (ld = M2, origin 0); WIN = true: a copy of a rectangle of it
-// (round 4 measured a per-tile LDS copy of the rectangle a tile's samples can
-// reach: slower, profiles/r04_tap_lds_ab.txt).  Same values either way, so
-// the same results.
-template <typename VP, bool WIN = false>
+// Where the bicubic reads the padded frame: cell (iy, ix) (1-based) starts at
+// element (iy - 1) + ld (ix - 1).  (Round 4 measured a per-tile LDS copy of
+// the rectangle a tile's samples can reach, read through a windowed view of
+// this kind: slower, profiles/r04_tap_lds_ab.txt -- not kept.)
+template <typename VP>
 struct TapView {
     VP p;
     uint32_t ld;
-    int r0, c0;
-    GQ_HD uint32_t cell(int iy, int ix) const
-    {
-        if constexpr (WIN) return (uint32_t)(iy - 1 - r0) + GQ_UMUL24(ld, ix - 1 - c0);
-        else return cell_elem(iy, ix, (int)ld);
-    }
+    GQ_HD uint32_t cell(int iy, int ix) const { return cell_elem(iy, ix, (int)ld); }
 };
 template <typename VP>
-GQ_HD TapView<VP, false> frame_view(VP VV, int M2)
+GQ_HD TapView<VP> frame_view(VP VV, int M2)
 {
-    return TapView<VP, false>{VV, (uint32_t)M2, 0, 0};
+    return TapView<VP>{VV, (uint32_t)M2};
 }
 
 // Elements of a padded-frame (VV) buffer: the (Mo+2) x (No+2) frame, then
