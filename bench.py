@@ -441,6 +441,7 @@ def run_c1(args, rank, world, local, barrier):
     # third on (scripts/c1_timing.py: first-use costs outside the kernels)
     for _ in range(min(args.warmup, 3)):
         gqmap_cpu(o, flo, seed=1, device=local)
+    settle = None if args.no_settle else settle_clocks(lambda: gqmap_cpu(o, flo, seed=1, device=local), args.steps)
     barrier()
     t0 = time.perf_counter()
     mu, sg, rou, tr = gqmap_cpu(o, flo, seed=0, device=local, return_trace=True)
@@ -449,7 +450,7 @@ def run_c1(args, rank, world, local, barrier):
     M, N, _ = flo.shape
     err = float(np.sqrt(((mu - flo) ** 2).sum(axis=2))[~unk].mean())
     return dict(elapsed=elapsed, pixels=M * N, nodes=M * N, aepe=err, flow=flo, unk=unk, mu=mu, opts=o, Mo=M, No=N,
-                its=tr.shape[0],
+                its=tr.shape[0], settle=settle,
                 workload=f"C1: {name} {N}x{M} legacy/gqmap_cpu.m flow denoising (input = GT flow, unknowns 0), "
                          f"K=9, var=gama=1, dta=inf, {args.steps} its, sigma0 = U+2 (seed 0); value includes the "
                          f"call's host<->device copies; aepe = mean |mu - flow|")
