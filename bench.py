@@ -338,7 +338,8 @@ def settle_clocks(run_chunk, chunk: int, min_s: float = 0.05, max_s: float = 1.0
     return {"iterations": chunk * len(times), "seconds": round(el, 4),
             "first_chunk_us_per_it": times[0] / chunk * 1e6, "last_chunk_us_per_it": times[-1] / chunk * 1e6,
             "note": "untimed: the hot path run until the GPU clocks settle (bench.settle_clocks); the timed "
-                    "steps still start from the seeded initial state at iteration 1"}
+                    "steps still start from the seeded initial state at iteration 1; cold_start_value: the same "
+                    "steps timed once before settling (right after the warm-up), for the record"}
 
 
 def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, extra, label):
@@ -355,7 +356,18 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     def chunk():
         eng.init_state(seed=rank)
         eng.run(20)
-    settle = settle_clocks(chunk, 20) if not args.no_settle else None
+    settle = None
+    if not args.no_settle:
+        # the same steps timed once before settling, for the record (the
+        # line's value is the settled run below)
+        eng.init_state(seed=rank)
+        barrier()
+        t0 = time.perf_counter()
+        eng.run(args.steps)
+        barrier()
+        cold = time.perf_counter() - t0
+        settle = settle_clocks(chunk, 20)
+        settle["cold_start_ms_per_step"] = cold / args.steps * 1e3
     eng.init_state(seed=rank)  # timed steps are iterations 1..steps of the solve
     barrier()
     t0 = time.perf_counter()
@@ -718,6 +730,10 @@ def main():
         }
         if r.get("settle"):
             out["clock_settle"] = r["settle"]
+            if "cold_start_ms_per_step" in r["settle"]:
+                # the same steps on rank 0 timed right after the warm-up, before settling
+                cs = r["settle"]["cold_start_ms_per_step"]
+                out["clock_settle"]["cold_start_value"] = units / (cs * 1e-3 * args.steps) / 1e9
         if cfg == "c1":
             # per pixel: node 2 x K x 6 flop, edges 4 x K^2 x ~40 flop (legacy/gqmap_cpu.m:20-54)
             fl = (2 * K * 6 + 4 * K * K * 40) * r["pixels"] * r["its"]
