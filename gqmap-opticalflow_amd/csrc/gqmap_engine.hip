@@ -97,6 +97,7 @@ constexpr int TS = TAB_STRIDE;
 constexpr int NPLANES = 9;
 constexpr int TRACE_CAP = 8192;
 constexpr int GRAPH_CHUNK = 50;
+constexpr int BAND_EVENTS = GRAPH_CHUNK;  // banded pipeline: events per band (launch_steps_banded)
 constexpr int NFIX = 5;        // fixed slots per block: Energy, sum|dmu_u|, sum|dsig_u|, #nonfinite, AEPE sum
 constexpr int ACC_SLICES = 8;
 constexpr int TRACE_W = 4;     // trace ring columns: Energy, ptdmu, ptdsigma, AEPE (NaN without a truth)
@@ -1799,7 +1800,9 @@ struct gqmap_ctx {
     int band_j = -1;  // set around a band launch (iter_params)
     int nbands = 0;   // streams / events created
     hipStream_t bstream[8] = {};
-    hipEvent_t bev[3][8] = {};
+    // one event per (iteration of a chunk, band): a stream capture must not
+    // re-record an event it has already used (HIP faulted at the first reuse)
+    hipEvent_t bev[BAND_EVENTS][8] = {};
     hipEvent_t bev_fork = nullptr;
     double *d_trace = nullptr;
     // pinned host mirrors: Ctl, the trace ring and the persistent failure
@@ -2622,17 +2625,23 @@ int band_count(const gqmap_ctx *c)
     return B;
 }
 
+// The band streams and events (outside any stream capture: capture_steps
+// calls it before it begins one).
+gqmap_status ensure_bands(gqmap_ctx *c, int B)
+{
+    for (int b = c->nbands; b < B; ++b) {
+        GQ_HIP(hipStreamCreateWithFlags(&c->bstream[b], hipStreamNonBlocking));
+        for (int r = 0; r < BAND_EVENTS; ++r) GQ_HIP(hipEventCreateWithFlags(&c->bev[r][b], hipEventDisableTiming));
+        c->nbands = b + 1;
+    }
+    if (!c->bev_fork) GQ_HIP(hipEventCreateWithFlags(&c->bev_fork, hipEventDisableTiming));
+    return GQMAP_OK;
+}
+
 gqmap_status launch_steps_banded(gqmap_ctx *c, int n, int B)
 {
     if (n <= 0) return GQMAP_OK;
-    if (c->nbands < B) {
-        for (int b = c->nbands; b < B; ++b) {
-            GQ_HIP(hipStreamCreateWithFlags(&c->bstream[b], hipStreamNonBlocking));
-            for (int r = 0; r < 3; ++r) GQ_HIP(hipEventCreateWithFlags(&c->bev[r][b], hipEventDisableTiming));
-        }
-        if (!c->bev_fork) GQ_HIP(hipEventCreateWithFlags(&c->bev_fork, hipEventDisableTiming));
-        c->nbands = B;
-    }
+    GQ_CHECK(c->nbands >= B && c->bev_fork, GQMAP_ERR_STATE, "band streams not created");
     hipStream_t main_stream = c->stream;
     k_band_base<<<1, 64, 0, main_stream>>>(c->d_ctl);
     GQ_HIP(hipEventRecord(c->bev_fork, main_stream));
@@ -2642,12 +2651,15 @@ gqmap_status launch_steps_banded(gqmap_ctx *c, int n, int B)
         for (int b = 0; b < B; ++b) {
             hipStream_t st = c->bstream[b];
             if (j > 0) {
-                if (b > 0) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 1) % 3][b - 1], 0));
-                if (b + 1 < B) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 1) % 3][b + 1], 0));
+                if (b > 0) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 1) % BAND_EVENTS][b - 1], 0));
+                if (b + 1 < B) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 1) % BAND_EVENTS][b + 1], 0));
             }
+            // (band b at j - 1 implies band b' finished j - 1 - |b - b'|:
+            // only bands three or more away need the explicit wait -- and a
+            // redundant wait inside a stream capture crashed HIP's capture)
             if (j > 1)
                 for (int b2 = 0; b2 < B; ++b2)
-                    if (b2 < b - 1 || b2 > b + 1) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 2) % 3][b2], 0));
+                    if (b2 < b - 2 || b2 > b + 2) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 2) % BAND_EVENTS][b2], 0));
             const int c0 = b * tn / B, c1 = (b + 1) * tn / B;
             TileSegs sg{};
             sg.lo[0] = c0 * tm;
@@ -2657,10 +2669,10 @@ gqmap_status launch_steps_banded(gqmap_ctx *c, int n, int B)
             launch_iter(c, &sg);
             c->stream = main_stream;
             c->band_j = -1;
-            GQ_HIP(hipEventRecord(c->bev[j % 3][b], st));
+            GQ_HIP(hipEventRecord(c->bev[j % BAND_EVENTS][b], st));
         }
     }
-    for (int b = 0; b < B; ++b) GQ_HIP(hipStreamWaitEvent(main_stream, c->bev[(n - 1) % 3][b], 0));
+    for (int b = 0; b < B; ++b) GQ_HIP(hipStreamWaitEvent(main_stream, c->bev[(n - 1) % BAND_EVENTS][b], 0));
     GQ_HIP(hipGetLastError());
     return GQMAP_OK;
 }
@@ -2670,7 +2682,11 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
 {
     c->ctl_known = false;
     if (launch_persist(c, n)) return GQMAP_OK;
-    if (const int B = band_count(c)) return launch_steps_banded(c, n, B);
+    if (const int B = band_count(c)) {
+        const gqmap_status sb = ensure_bands(c, B);  // no-op after the first call
+        if (sb != GQMAP_OK) return sb;
+        return launch_steps_banded(c, n, B);
+    }
     gqmap_status st = GQMAP_OK;
     for (int i = 0; i < n && st == GQMAP_OK; ++i) st = launch_step(c);
     if (st == GQMAP_OK && rccl_spec(c)) st = join_spec(c);
@@ -2781,6 +2797,10 @@ gqmap_status capture_steps(gqmap_ctx *c, int n, hipGraphExec_t *out)
 {
     if (*out) return GQMAP_OK;
     (void)launch_persist(c, n, true);  // occupancy query, snapshot buffers: outside the capture
+    if (const int B = band_count(c)) {
+        const gqmap_status sb = ensure_bands(c, B);
+        if (sb != GQMAP_OK) return sb;
+    }
     hipGraph_t g;
     GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     gqmap_status st = launch_steps(c, n);
@@ -3334,7 +3354,9 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         int left = chunk;
         c->ctl_known = false;
         static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
-        if (!no_graph) {
+        // (the banded pipeline launches directly: a stream capture of its
+        // cross-stream event waits faulted inside HIP beyond two iterations)
+        if (!no_graph && band_count(c) == 0) {
             // GRAPH_CHUNK-iteration graphs, then the remainder as graphs of
             // 2^k iterations (a short run replays graphs too)
             if (left >= GRAPH_CHUNK && (s = ensure_graph(c)) != GQMAP_OK) return s;
@@ -3432,6 +3454,7 @@ gqmap_status gqmap_prepare(gqmap_ctx *c)
              "tile %d/%d: attach RCCL (gqmap_tile_attach_rccl) or use gqmap_tile_group_run", c->tile,
              c->n_tiles);
     DeviceGuard dg(c->device);
+    if (const int B = band_count(c)) return ensure_bands(c, B);  // launched directly, no graphs
     gqmap_status s = ensure_graph(c);
     if (s != GQMAP_OK) return s;
     GQ_HIP(hipGraphUpload(c->graph, c->stream));
@@ -3887,7 +3910,7 @@ void gqmap_destroy(gqmap_ctx *c)
         if (st) (void)hipStreamDestroy(st);
     for (int b = 0; b < c->nbands; ++b) {
         (void)hipStreamSynchronize(c->bstream[b]);
-        for (int r = 0; r < 3; ++r) (void)hipEventDestroy(c->bev[r][b]);
+        for (int r = 0; r < BAND_EVENTS; ++r) (void)hipEventDestroy(c->bev[r][b]);
         (void)hipStreamDestroy(c->bstream[b]);
     }
     if (c->bev_fork) (void)hipEventDestroy(c->bev_fork);

@@ -40,7 +40,7 @@ for prec in ("fp64", "fp32"):
             out = subprocess.run([sys.executable, "-c", CODE, prec], cwd=ROOT, env=env, capture_output=True,
                                  text=True, timeout=300)
             if out.returncode != 0:
-                print(f"{prec} B={b} FAILED {out.stderr[-1500:]}", flush=True)
+                print(f"{prec} B={b} FAILED rc={out.returncode} {out.stdout[-500:]} {out.stderr[-1500:]}", flush=True)
                 sys.exit(1)
             a, bb, chk = out.stdout.split()
             print(f"{prec} rep {rep} B={b}: run(20) {a} us/it, run(100) {bb} us/it, {chk}", flush=True)
