@@ -97,7 +97,6 @@ constexpr int TS = TAB_STRIDE;
 constexpr int NPLANES = 9;
 constexpr int TRACE_CAP = 8192;
 constexpr int GRAPH_CHUNK = 50;
-constexpr int BAND_EVENTS = GRAPH_CHUNK;  // banded pipeline: events per band (launch_steps_banded)
 constexpr int NFIX = 5;        // fixed slots per block: Energy, sum|dmu_u|, sum|dsig_u|, #nonfinite, AEPE sum
 constexpr int ACC_SLICES = 8;
 constexpr int TRACE_W = 4;     // trace ring columns: Energy, ptdmu, ptdsigma, AEPE (NaN without a truth)
@@ -125,16 +124,6 @@ struct Ctl {
     alignas(128) int it_i;
     int done_i;
     double T_i;
-    // banded pipeline (launch_steps_banded): the chunk's first iteration as
-    // k_band_base froze it (band launch j runs iteration it_b + j from state
-    // parity done_b + j), and the second ticket / accumulator slot -- the
-    // launches of iterations j and j + 1 overlap, so odd iterations count and
-    // add here while even ones use arrive / acc
-    alignas(128) int it_b;
-    int done_b;
-    double T_b;
-    alignas(128) int arrive1;
-    unsigned long long acc1[ACC_SLICES][NFIX + GQMAP_LMAX][4];
 };
 
 struct FinParams {
@@ -204,7 +193,6 @@ struct IterParams {
     int64_t MNL;
     unsigned *bar;  // k_iter_persist: barrier counters (BAR_WORDS, zero between launches)
     int spec;       // speculative RCCL tile: run iteration Ctl::it_i / done_i / T_i
-    int band_j;     // >= 0: a band launch of the chunk's iteration band_j (launch_steps_banded)
 };
 
 // Quadrature tables are read with wave-uniform indices; routing them through
@@ -356,8 +344,7 @@ __device__ __forceinline__ void acc_add_agent(unsigned long long *acc4, fix128 v
 }
 // The last workgroup: Ctl::acc -> tot[] (LDS), then clear acc for the next
 // iteration.  All 256 threads call it.
-__device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long long *sh,
-                               unsigned long long *acc_base = nullptr)
+__device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long long *sh)
 {
     const int NPR = F.L > 1 ? NFIX + F.L : NFIX;
     const int tid = threadIdx.x;
@@ -365,7 +352,7 @@ __device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long lo
     if (tid < 4 * NPR) {
         // all slices' loads in flight together, then the clears (one memory
         // round trip instead of eight: finalize 2.9 -> ~1 us)
-        unsigned long long *a = (acc_base ? acc_base : &F.ctl->acc[0][0][0]) + tid;
+        unsigned long long *a = &F.ctl->acc[0][0][0] + tid;
         unsigned long long v[ACC_SLICES];
 #pragma unroll
         for (int x = 0; x < ACC_SLICES; ++x) v[x] = __hip_atomic_load(a + x * SL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1034,35 +1021,10 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1))
             v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
         if (P.fused || P.tile_acc) {
-            // banded pipeline: odd iterations of the chunk into the second slot
-            auto &acc = (P.band_j >= 0 && (P.band_j & 1)) ? ctl->acc1 : ctl->acc;
-            if (v != 0) acc_add_agent(&acc[blockIdx.x % ACC_SLICES][tid][0], v);
+            if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
         } else {
             store_part_agent(P.partials, P.fin.nblocks, part_r, tid, v);
         }
-    }
-}
-
-// Banded pipeline: the temperature of the chunk's iteration it_b + j --
-// fin_apply's decay after every iteration t with t % t_decay_every == 0, from
-// the chunk's frozen T_b (L = 1: nothing else of the finalize feeds the next
-// iteration).
-__device__ __forceinline__ double band_T(const Ctl *ctl, const FinParams &F, int j)
-{
-    double T = ctl->T_b;
-    if (F.t_decay_every > 0)
-        for (int t = ctl->it_b; t < ctl->it_b + j; ++t)
-            if (t % F.t_decay_every == 0) T = fmax(T * F.drate, F.t_min);
-    return T;
-}
-
-// Freezes the chunk's first iteration for the band launches (one thread).
-__global__ void k_band_base(Ctl *ctl)
-{
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        ctl->it_b = ctl->it;
-        ctl->done_b = ctl->done;
-        ctl->T_b = ctl->T;
     }
 }
 
@@ -1095,16 +1057,16 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
     __shared__ TileLdsQ<R, Q> lds;
     const int part_r = P.part_off + b;
-    const bool banded = P.band_j >= 0;
-    const int it_run = banded ? ctl->it_b + P.band_j : P.spec ? ctl->it_i : ctl->it;
-    const int par_run = (banded ? ctl->done_b + P.band_j : P.spec ? ctl->done_i : ctl->done) & 1;
-    const double T_run = banded ? band_T(ctl, P.fin, P.band_j) : P.spec ? ctl->T_i : ctl->T;
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
     } else if (edge_first)
-        iter_tile<R, VT, ENG, Q, true, false, NT>(P, tile, it_run, par_run, part_r, lds, l0, l1, T_run, false);
+        iter_tile<R, VT, ENG, Q, true, false, NT>(P, tile, P.spec ? ctl->it_i : ctl->it,
+                                                  (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
+                                                  P.spec ? ctl->T_i : ctl->T, false);
     else
-        iter_tile<R, VT, ENG, Q, false, false, NT>(P, tile, it_run, par_run, part_r, lds, l0, l1, T_run, false);
+        iter_tile<R, VT, ENG, Q, false, false, NT>(P, tile, P.spec ? ctl->it_i : ctl->it,
+                                                   (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
+                                                   P.spec ? ctl->T_i : ctl->T, false);
 #if GQ_TIMELINE
     __syncthreads();
     TL_STAMP(0, tl0);
@@ -1125,14 +1087,10 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     // write through this XCD's L2; once wave 0 has seen them complete it
     // takes the arrival ticket.  No L2 write-back or invalidate: a fence here
     // costs every workgroup (measured +20..70 us per iteration on C2).
-    // (banded pipeline: the ticket of the chunk iteration's slot counts the
-    // workgroups of all its band launches)
-    const bool odd = banded && (P.band_j & 1);
-    int *arrive = odd ? &ctl->arrive1 : &ctl->arrive;
     __shared__ int last;
     if (tid == 0) {
         __builtin_amdgcn_s_waitcnt(0);
-        last = atomicAdd(arrive, 1) == (banded ? P.ticket_total : (int)gridDim.x) - 1;
+        last = atomicAdd(&ctl->arrive, 1) == (int)gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
@@ -1143,15 +1101,13 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
 #endif
     __shared__ double tot[NFIX + GQMAP_LMAX];
     __shared__ unsigned long long sh_acc[4 * (NFIX + GQMAP_LMAX)];
-    fin_reduce_acc(P.fin, tot, sh_acc, odd ? &ctl->acc1[0][0][0] : &ctl->acc[0][0][0]);
+    fin_reduce_acc(P.fin, tot, sh_acc);
 #if GQ_TIMELINE
     if (tl_on) tl_row[9] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (tid == 0) {
-        // banded: iteration j + 1 may have run before finalize(j) met the
-        // stop rule -- its sums are dropped, Ctl keeps pointing at state j
-        if (!(banded && ctl->stop)) fin_apply(P.fin, tot);
-        *arrive = 0;
+        fin_apply(P.fin, tot);
+        ctl->arrive = 0;
 #if GQ_TIMELINE
         if (tl_on) tl_row[7] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1794,16 +1750,6 @@ struct gqmap_ctx {
     Ctl *d_snap_ctl = nullptr;
     size_t snap_bytes = 0;
     bool persist_off = false;
-    // banded pipeline (launch_steps_banded): column bands of tiles on their
-    // own streams, iteration j + 1 of a band as soon as its neighbours are done
-    // with iteration j
-    int band_j = -1;  // set around a band launch (iter_params)
-    int nbands = 0;   // streams / events created
-    hipStream_t bstream[8] = {};
-    // one event per (iteration of a chunk, band): a stream capture must not
-    // re-record an event it has already used (HIP faulted at the first reuse)
-    hipEvent_t bev[BAND_EVENTS][8] = {};
-    hipEvent_t bev_fork = nullptr;
     double *d_trace = nullptr;
     // pinned host mirrors: Ctl, the trace ring and the persistent failure
     // word, read back together at the end of a run chunk (one sync)
@@ -2071,8 +2017,6 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     fix128 *gt = c->gbuf ? c->gbuf : c->d_gathered;
     P.tile_totals = gt ? gt + (size_t)c->tile * (NFIX + c->L) : nullptr;
     P.spec = c->spec_now ? 1 : 0;
-    P.band_j = c->band_j;
-    if (c->band_j >= 0) P.ticket_total = c->nblocks;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
     P.band_rows = 0;
@@ -2604,89 +2548,11 @@ gqmap_status launch_step(gqmap_ctx *c)
     return launch_tail(c);
 }
 
-// Banded pipeline: B column bands of tiles, one stream each.  Band b's launch
-// of iteration j waits for bands b - 1 and b + 1 to finish iteration j - 1
-// (the state it reads; its own previous launch is stream-ordered) and for all
-// bands to finish iteration j - 2 (whose finalize freed the ticket / sum slot
-// iteration j reuses, and judged the stop rule: at most two iterations are in
-// flight, as in the speculative step).  Every launch runs iteration
-// Ctl::it_b + j (k_band_base freezes the chunk's start); the last workgroup of
-// iteration j over all bands runs its finalize.  Same tiles, same arithmetic,
-// same bits as one launch per iteration.  Whole grid, L = 1, Q = 1..16 only;
-// GQMAP_BANDS=B (3..8) turns it on.
-int band_count(const gqmap_ctx *c)
-{
-    static const char *e = std::getenv("GQMAP_BANDS");
-    const int B = e ? std::atoi(e) : 0;
-    if (B < 3 || B > 8) return 0;
-    if (c->comm || c->host_xfer || c->n_tiles != 1 || c->in_group || c->L != 1) return 0;
-    if (c->kq < 1 || c->kq > 16) return 0;
-    if (c->tiles_n < B) return 0;
-    return B;
-}
-
-// The band streams and events (outside any stream capture: capture_steps
-// calls it before it begins one).
-gqmap_status ensure_bands(gqmap_ctx *c, int B)
-{
-    for (int b = c->nbands; b < B; ++b) {
-        GQ_HIP(hipStreamCreateWithFlags(&c->bstream[b], hipStreamNonBlocking));
-        for (int r = 0; r < BAND_EVENTS; ++r) GQ_HIP(hipEventCreateWithFlags(&c->bev[r][b], hipEventDisableTiming));
-        c->nbands = b + 1;
-    }
-    if (!c->bev_fork) GQ_HIP(hipEventCreateWithFlags(&c->bev_fork, hipEventDisableTiming));
-    return GQMAP_OK;
-}
-
-gqmap_status launch_steps_banded(gqmap_ctx *c, int n, int B)
-{
-    if (n <= 0) return GQMAP_OK;
-    GQ_CHECK(c->nbands >= B && c->bev_fork, GQMAP_ERR_STATE, "band streams not created");
-    hipStream_t main_stream = c->stream;
-    k_band_base<<<1, 64, 0, main_stream>>>(c->d_ctl);
-    GQ_HIP(hipEventRecord(c->bev_fork, main_stream));
-    for (int b = 0; b < B; ++b) GQ_HIP(hipStreamWaitEvent(c->bstream[b], c->bev_fork, 0));
-    const int tm = c->tiles_m, tn = c->tiles_n;
-    for (int j = 0; j < n; ++j) {
-        for (int b = 0; b < B; ++b) {
-            hipStream_t st = c->bstream[b];
-            if (j > 0) {
-                if (b > 0) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 1) % BAND_EVENTS][b - 1], 0));
-                if (b + 1 < B) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 1) % BAND_EVENTS][b + 1], 0));
-            }
-            // (band b at j - 1 implies band b' finished j - 1 - |b - b'|:
-            // only bands three or more away need the explicit wait -- and a
-            // redundant wait inside a stream capture crashed HIP's capture)
-            if (j > 1)
-                for (int b2 = 0; b2 < B; ++b2)
-                    if (b2 < b - 2 || b2 > b + 2) GQ_HIP(hipStreamWaitEvent(st, c->bev[(j - 2) % BAND_EVENTS][b2], 0));
-            const int c0 = b * tn / B, c1 = (b + 1) * tn / B;
-            TileSegs sg{};
-            sg.lo[0] = c0 * tm;
-            sg.n[0] = (c1 - c0) * tm;
-            c->stream = st;
-            c->band_j = j;
-            launch_iter(c, &sg);
-            c->stream = main_stream;
-            c->band_j = -1;
-            GQ_HIP(hipEventRecord(c->bev[j % BAND_EVENTS][b], st));
-        }
-    }
-    for (int b = 0; b < B; ++b) GQ_HIP(hipStreamWaitEvent(main_stream, c->bev[(n - 1) % BAND_EVENTS][b], 0));
-    GQ_HIP(hipGetLastError());
-    return GQMAP_OK;
-}
-
 // n iterations: one persistent launch for small ctf grids, else n steps
 gqmap_status launch_steps(gqmap_ctx *c, int n)
 {
     c->ctl_known = false;
     if (launch_persist(c, n)) return GQMAP_OK;
-    if (const int B = band_count(c)) {
-        const gqmap_status sb = ensure_bands(c, B);  // no-op after the first call
-        if (sb != GQMAP_OK) return sb;
-        return launch_steps_banded(c, n, B);
-    }
     gqmap_status st = GQMAP_OK;
     for (int i = 0; i < n && st == GQMAP_OK; ++i) st = launch_step(c);
     if (st == GQMAP_OK && rccl_spec(c)) st = join_spec(c);
@@ -2797,10 +2663,6 @@ gqmap_status capture_steps(gqmap_ctx *c, int n, hipGraphExec_t *out)
 {
     if (*out) return GQMAP_OK;
     (void)launch_persist(c, n, true);  // occupancy query, snapshot buffers: outside the capture
-    if (const int B = band_count(c)) {
-        const gqmap_status sb = ensure_bands(c, B);
-        if (sb != GQMAP_OK) return sb;
-    }
     hipGraph_t g;
     GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     gqmap_status st = launch_steps(c, n);
@@ -3354,9 +3216,7 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         int left = chunk;
         c->ctl_known = false;
         static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
-        // (the banded pipeline launches directly: a stream capture of its
-        // cross-stream event waits faulted inside HIP beyond two iterations)
-        if (!no_graph && band_count(c) == 0) {
+        if (!no_graph) {
             // GRAPH_CHUNK-iteration graphs, then the remainder as graphs of
             // 2^k iterations (a short run replays graphs too)
             if (left >= GRAPH_CHUNK && (s = ensure_graph(c)) != GQMAP_OK) return s;
@@ -3454,7 +3314,6 @@ gqmap_status gqmap_prepare(gqmap_ctx *c)
              "tile %d/%d: attach RCCL (gqmap_tile_attach_rccl) or use gqmap_tile_group_run", c->tile,
              c->n_tiles);
     DeviceGuard dg(c->device);
-    if (const int B = band_count(c)) return ensure_bands(c, B);  // launched directly, no graphs
     gqmap_status s = ensure_graph(c);
     if (s != GQMAP_OK) return s;
     GQ_HIP(hipGraphUpload(c->graph, c->stream));
@@ -3908,12 +3767,6 @@ void gqmap_destroy(gqmap_ctx *c)
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t st : {c->side, c->bnd, c->fin})
         if (st) (void)hipStreamDestroy(st);
-    for (int b = 0; b < c->nbands; ++b) {
-        (void)hipStreamSynchronize(c->bstream[b]);
-        for (int r = 0; r < BAND_EVENTS; ++r) (void)hipEventDestroy(c->bev[r][b]);
-        (void)hipStreamDestroy(c->bstream[b]);
-    }
-    if (c->bev_fork) (void)hipEventDestroy(c->bev_fork);
     if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);

@@ -527,75 +527,3 @@ np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigu.ravel(), 
             subprocess.run([sys.executable, "-c", code, f, precision], cwd=root, env=env, check=True, timeout=300)
             outs.append(np.load(f))
     np.testing.assert_array_equal(outs[0], outs[1])
-
-
-_BANDED_CODE = r'''
-import sys, dataclasses, numpy as np
-sys.path.insert(0, ".")
-from tests.test_gpu_parity import _reference_init_case
-from gqmap_opticalflow_amd import Engine
-prec, split, tor, pre = sys.argv[2], int(sys.argv[3]), float(sys.argv[4]), int(sys.argv[5])
-I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 128, 160, 100, 150, L=1, K=9, split=split,
-                                           t_decay_every=20)
-o = dict(o, temperature=0.3)
-st = dataclasses.replace(st, T=0.3)
-if pre:  # start from a later state (no stop rule on the way there)
-    with Engine(dict(o, tor=0.0), I1, I2, "mixture", prec) as e:
-        e.set_state(st)
-        e.run(pre)
-        st = e.get_state()
-with Engine(dict(o, tor=tor), I1, I2, "mixture", prec) as e:
-    e.set_state(st)
-    d1, t1 = e.run(130)      # two 50-iteration chunks + 30 more
-    d2, t2 = e.run(7)        # a short run after them
-    g = e.get_state()
-    info = e.info()
-t1 = np.vstack([t1, np.full((130 - t1.shape[0], 3), np.nan)])
-np.save(sys.argv[1], np.concatenate([[d1, d2, g.it, g.T, info.stopped], t1.ravel(), t2.ravel(), g.muu.ravel(),
-                                     g.muv.ravel(), g.sigu.ravel(), g.sigv.ravel(), g.pn.ravel(), g.rou.ravel()]))
-'''
-
-
-def _banded_runs(variants, precision, split, tor, pre):
-    import subprocess
-    import sys
-    import tempfile
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    outs = []
-    with tempfile.TemporaryDirectory() as d:
-        for v in variants:
-            env = {k: x for k, x in os.environ.items() if k != "GQMAP_BANDS"}
-            if v:
-                env["GQMAP_BANDS"] = v
-            f = os.path.join(d, f"b{v}.npy")
-            subprocess.run([sys.executable, "-c", _BANDED_CODE, f, precision, str(split), repr(tor), str(pre)],
-                           cwd=root, env=env, check=True, timeout=300)
-            outs.append(np.load(f, allow_pickle=False))
-    return outs
-
-
-@pytest.mark.parametrize("precision,split,stop", [("fp64", 1, False), ("fp32", 1, False), ("fp64", 4, False),
-                                                  ("fp64", 1, True)])
-def test_banded_pipeline_same_bits(precision, split, stop):
-    # GQMAP_BANDS (launch_steps_banded: column bands on their own streams,
-    # iteration j + 1 of a band overlapping iteration j of the bands that are
-    # not its neighbours) is a schedule: the same trace, state, iteration
-    # count and temperature as one launch per iteration, with the temperature
-    # decaying inside the chunks.  stop: from the state after 130 iterations,
-    # a threshold the solve first meets inside a chunk (a new running minimum
-    # of ptdmu), so the band launches of the iteration after the stopping one
-    # are already in flight when the verdict comes
-    tor, pre = 0.0, 0
-    if stop:
-        pre = 130
-        ptd = _banded_runs([None], precision, split, 0.0, pre)[0][5:5 + 3 * 130].reshape(130, 3)[:, 1]
-        recs = [k for k in range(5, 125) if ptd[k] < ptd[:k].min()]
-        if not recs:
-            pytest.skip("ptdmu sets no new minimum inside the window")
-        k = recs[-1]
-        tor = float(ptd[:k].min())  # ptd[j] < tor first at j = k
-    outs = _banded_runs([None, "4", "3"], precision, split, tor, pre)
-    if stop:
-        assert outs[0][0] == k + 1 and outs[0][4] == 1
-    for o in outs[1:]:
-        np.testing.assert_array_equal(outs[0], o)
