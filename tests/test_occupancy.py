@@ -1,0 +1,56 @@
+"""Waves-per-SIMD guard on the built library (no GPU): the headline kernels
+sit on register thresholds (MI355X: <= 128 VGPRs -> 4 waves per SIMD, <= 168
+-> 3, <= 256 -> 2).  Round 4 measured what crossing one costs: two extra
+VGPRs on the C2 fp64 kernel (168 -> 170, 3 -> 2 waves) made it 9% slower
+(profiles/r04_banded_pipeline.txt).  Reads .vgpr_count / .agpr_count from
+the gfx950 code object's metadata in gqmap-opticalflow_amd/libgqmap.so."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "gqmap-opticalflow_amd", "libgqmap.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+# kernel (mangled) -> max VGPRs (agpr 0): C2 fp64 (3 waves), C2 fp32 (4), C3's
+# full level (3), its 240x320 level and C4 (2, no accumulation registers)
+LIMITS = {
+    "_ZN2gq6k_iterIdfLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE": 168,
+    "_ZN2gq6k_iterIdfLi0ELi1ELb1EEEvNS_10IterParamsIT_T0_EE": 168,
+    "_ZN2gq6k_iterIffLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE": 128,
+    "_ZN2gq6k_iterIdfLi2ELi1ELb0EEEvNS_10IterParamsIT_T0_EE": 168,
+    "_ZN2gq6k_iterIddLi2ELi2ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
+    "_ZN2gq6k_iterIdfLi1ELi4ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
+}
+
+
+def _kernel_registers(tmp):
+    fat = os.path.join(tmp, "fatbin.bin")
+    co = os.path.join(tmp, "co.elf")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", LIB, os.path.join(tmp, "x.so")],
+                   check=True, capture_output=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                           text=True).stdout
+    regs = {}
+    for block in re.split(r"\n  - ", notes):
+        name = re.search(r"\n\s*\.name:\s+(\S+)", "\n" + block)
+        v = re.search(r"\.vgpr_count:\s+(\d+)", block)
+        a = re.search(r"\.agpr_count:\s+(\d+)", block)
+        if name and v:
+            regs[name.group(1)] = (int(v.group(1)), int(a.group(1)) if a else 0)
+    return regs
+
+
+@pytest.mark.skipif(not os.path.exists(LIB) or not shutil.which(f"{LLVM}/llvm-readelf"),
+                    reason="library or ROCm LLVM tools absent")
+def test_headline_kernels_keep_their_waves(tmp_path):
+    regs = _kernel_registers(str(tmp_path))
+    for name, limit in LIMITS.items():
+        assert name in regs, name
+        v, a = regs[name]
+        assert v <= limit and a == 0, f"{name}: {v} VGPRs + {a} AGPRs > {limit}"
