@@ -31,6 +31,11 @@ named in `config`):
                   (strong scaling of the headline pair)
     --config c1   Dimetrodon 388x584 legacy/gqmap_cpu.m flow denoising, 50 its
                   (device drop-in; timed call includes its host<->device copies)
+Before the timed steps (after --warmup W steps and the graph capture) the
+hot path runs untimed until the GPU clocks settle (settle_clocks; reported as
+`clock_settle`, with the same steps timed once cold as `cold_start_value`;
+--no-settle skips it): a 20-step window started cold measures the clock ramp
+(profiles/r04_clock_ramp.txt).
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
