@@ -209,6 +209,21 @@ def cpu_baseline(I1, I2, opts, engine="mixture", label="", budget_s: float = 6.0
                       f"{t_ema:.1f}s"}
 
 
+def _pix_stats(a, b, o):
+    """Pixels whose flow differs by more than 1e-9 (either component), and
+    pixels whose mean sits on OPPOSITE clamp bounds of
+    gqmap_gpu_mixture.m:41-42 in the two flows (|du| = maxu - minu or
+    |dv| = maxv - minv)."""
+    du, dv = np.abs(a[:, :, 0] - b[:, :, 0]), np.abs(a[:, :, 1] - b[:, :, 1])
+    diff = int(((du > 1e-9) | (dv > 1e-9)).sum())
+    flip = int(((du == o["maxu"] - o["minu"]) | (dv == o["maxv"] - o["minv"])).sum())
+    return diff, flip
+
+
+def _first_flip(flips):
+    return next((i + 1 for i, f in enumerate(flips) if f > 0), None)
+
+
 def parity_gate(r, engine, steps, precision, split, seed):
     """The north-star gate (BASELINE.md:64-65), after the timed region: the
     same `steps` iterations from the same seeded init on the CPU -- the CPU
@@ -217,7 +232,18 @@ def parity_gate(r, engine, steps, precision, split, seed):
     reference (oracle/gqmap_oracle.c: aepe_delta_literal against the 1e-4
     gate) -- then AEPE (gqmap_gpu_mixture.m:63-64) and flowToColor
     (gqmap_gpu_mixture.m:60; uint8 pixels that differ) of each CPU flow
-    against the GPU's."""
+    against the GPU's.
+
+    Single-Gaussian mixture (C2) adds two records:
+      * `divergence`: the literal restatement run against ITSELF with mu_u
+        perturbed by +-1e-13 (aepe_spread_literal = the larger |AEPE delta|),
+        and per iteration (the first TRACK_ITS) the pixels whose flow differs
+        by > 1e-9 and the pixels on opposite clamp bounds, for GPU vs
+        literal and literal vs perturbed literal, with the first iteration a
+        bound flip appears in each;
+      * `literal_engine`: the literal-order engine's flow (arith="literal")
+        against the literal restatement run with the engine's Gauss-Hermite
+        rule -- bit-identical (aepe_delta_literal 0.0, colour mismatch 0)."""
     from gqmap_opticalflow_amd import aepe, flow_to_color, gauss_hermite, initial_state
     from oracle import oracle
     I1, I2, opts, mp_gpu, flo, unk = r["I1"], r["I2"], r["opts"], r["map"], r["flo"], r["unk"]
@@ -240,18 +266,73 @@ def parity_gate(r, engine, steps, precision, split, seed):
         f = up(f)
         return f[4:-4, 4:-4] if sup else f
 
+    def seeded(pert=0.0):
+        st0 = initial_state(o, M, N, seed=seed, engine=engine)
+        return oracle.State(st0.muu + pert, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha), st0.T
+
     img_gpu = flow_to_color(colour(mp_gpu))[0]
     a_gpu = aepe(flo, up(mp_gpu), unk, crop)
     out = {"its": steps, "threads": threads, "gate": 1e-4, "aepe_gpu": a_gpu}
-    for kind in ("emul", "literal"):
-        st0 = initial_state(o, M, N, seed=seed, engine=engine)
-        st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
+    stepped = engine == "mixture" and L == 1 and r.get("maps_it") is not None
+    finals = {}
+    if stepped:
+        # the literal restatement one iteration at a time (same arithmetic as
+        # one call): unperturbed, mu_u +- 1e-13, and with the engine's rule
         t0 = time.perf_counter()
-        if kind == "emul":
-            done, _, _ = oracle.emu_run(o, I1, I2, st, 1, steps, X, W, T=st0.T, nthreads=threads,
-                                        fp32=precision == "fp32", split=split)
+        runs = {"lit": seeded(), "lit_p": seeded(1e-13), "lit_m": seeded(-1e-13)}
+        if r.get("literal") is not None and "map" in r["literal"]:
+            runs["lit_rule"] = seeded()
+        maps_it = r["maps_it"]
+        traj = {k: {"diff": [], "flip": []} for k in ("gpu_vs_literal", "literal_vs_literal+1e-13",
+                                                       "literal_vs_literal-1e-13")}
+        for it in range(1, steps + 1):
+            for k, (st, T) in runs.items():
+                kw = dict(X=X, W=W) if k == "lit_rule" else {}
+                oracle.run(o, I1, I2, st, it, 1, T=T, nthreads=threads, **kw)
+            if it <= len(maps_it):
+                lm = cpu_map(runs["lit"][0], False)
+                for key, other in (("gpu_vs_literal", maps_it[it - 1]),
+                                   ("literal_vs_literal+1e-13", cpu_map(runs["lit_p"][0], False)),
+                                   ("literal_vs_literal-1e-13", cpu_map(runs["lit_m"][0], False))):
+                    d, f = _pix_stats(other, lm, o)
+                    traj[key]["diff"].append(d)
+                    traj[key]["flip"].append(f)
+        finals["literal"] = runs["lit"][0]
+        a_lit = aepe(flo, cpu_map(runs["lit"][0], False), unk, crop)
+        a_p = aepe(flo, cpu_map(runs["lit_p"][0], False), unk, crop)
+        a_m = aepe(flo, cpu_map(runs["lit_m"][0], False), unk, crop)
+        for v in traj.values():
+            v["first_flip_iteration"] = _first_flip(v["flip"])
+        out["divergence"] = {
+            "tracked_iterations": len(maps_it), "diff_threshold": 1e-9,
+            "flip": "pixels whose mean sits on opposite clamp bounds (|dmu_u| = maxu-minu or |dmu_v| = maxv-minv, "
+                    "gqmap_gpu_mixture.m:41-42) in the two flows",
+            "aepe_literal": a_lit, "aepe_literal_plus_1e-13": a_p, "aepe_literal_minus_1e-13": a_m,
+            "trajectories": traj, "cpu_s": time.perf_counter() - t0}
+        out["aepe_spread_literal"] = max(abs(a_p - a_lit), abs(a_m - a_lit))
+        if "lit_rule" in runs:
+            lm = cpu_map(runs["lit_rule"][0], False)
+            lg = r["literal"]["map"]
+            a_lg, a_lr = aepe(flo, lg, unk, crop), aepe(flo, lm, unk, crop)
+            out["literal_engine"] = {
+                "aepe_gpu": a_lg, "aepe_cpu_literal": a_lr, "aepe_delta_literal": a_lg - a_lr,
+                "flow_bit_exact": bool(np.array_equal(lg, lm)),
+                "flow_max_abs_diff": float(np.max(np.abs(lg - lm))),
+                "colour_mismatch_literal": int(np.any(oracle.flow_to_color(lm)[0] != flow_to_color(lg)[0],
+                                                      axis=2).sum()),
+                "note": "GPU arith=literal vs oracle/gqmap_oracle.c with the engine's Gauss-Hermite rule (the "
+                        "restatement's own eig rule differs by a few ulps: aepe_delta_literal above uses it)"}
+    for kind in ("emul", "literal"):
+        t0 = time.perf_counter()
+        if kind in finals:
+            st, done = finals[kind], steps
         else:
-            done, _, _ = oracle.run(o, I1, I2, st, 1, steps, T=st0.T, nthreads=threads)
+            st, T0 = seeded()
+            if kind == "emul":
+                done, _, _ = oracle.emu_run(o, I1, I2, st, 1, steps, X, W, T=T0, nthreads=threads,
+                                            fp32=precision == "fp32", split=split)
+            else:
+                done, _, _ = oracle.run(o, I1, I2, st, 1, steps, T=T0, nthreads=threads)
         mp = cpu_map(st, det_exp=kind == "emul")
         a = aepe(flo, up(mp), unk, crop)
         img = oracle.flow_to_color(colour(mp))[0]
@@ -263,9 +344,8 @@ def parity_gate(r, engine, steps, precision, split, seed):
         if done != steps:
             out[f"error_{kind}"] = f"stopped after {done}/{steps}"
     if "map1" in r:  # per-step agreement: iteration 1 alone, GPU vs the literal restatement
-        st0 = initial_state(o, M, N, seed=seed, engine=engine)
-        st = oracle.State(st0.muu, st0.muv, st0.sigu, st0.sigv, st0.pn, st0.rou, st0.w, st0.alpha)
-        oracle.run(o, I1, I2, st, 1, 1, T=st0.T, nthreads=threads)
+        st, T0 = seeded()
+        oracle.run(o, I1, I2, st, 1, 1, T=T0, nthreads=threads)
         mp1 = cpu_map(st, det_exp=False)
         out["it1_flow_max_abs_diff_literal"] = float(np.max(np.abs(mp1 - r["map1"])))
         out["it1_aepe_delta_literal"] = aepe(flo, up(r["map1"]), unk, crop) - aepe(flo, up(mp1), unk, crop)
@@ -277,7 +357,8 @@ def parity_gate(r, engine, steps, precision, split, seed):
     out["note"] = ("emul: the CPU model sharing the kernel's arithmetic spec (gqmap_math.h) -- bit-exact at any "
                    "number of iterations; literal: the fp64 restatement of the MATLAB, which differs by a rounding "
                    "or two per operation -- the solver's transient is chaotic, so that difference grows with the "
-                   "iteration count (DESIGN.md 2)")
+                   "iteration count (DESIGN.md 2; divergence: the same growth between the restatement and itself "
+                   "under a 1e-13 perturbation); literal_engine: the engine run in the reference's operation order")
     return out
 
 
@@ -409,16 +490,78 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
         a = aepe(flo, mp, unk)
     nodes = eng.M * eng.N
     split = eng.info().split
+    # the flow after each of the first track_its iterations (the parity
+    # gate's divergence trajectory against the literal restatement)
+    maps_it = []
+    if rank == 0 and engine == "mixture" and L == 1 and not args.no_parity:
+        eng.init_state(seed=rank)
+        for _ in range(min(gate_its, TRACK_ITS)):
+            eng.run(1)
+            maps_it.append(eng.map())
     eng.close()
+    lit = None
+    if engine == "mixture" and args.precision == "fp64" and not args.no_literal:
+        try:
+            lit = literal_engine_leg(args, rank, barrier, opts, I1, I2, flo, unk, gate_its, local)
+        except Exception as e:  # reported in the line; the headline value stands
+            lit = {"error": f"{type(e).__name__}: {e}"[:300]}
     Mo, No = I1.shape
     ksuf = {"mixture": 0, "super": 1}[engine]
     R = "double" if args.precision == "fp64" else "float"
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, instrumented_ms=total_ms, pixels=Mo * No, nodes=nodes, aepe=a, name=name,
-                settle=settle,
+                settle=settle, maps_it=maps_it, literal=lit,
                 I1=I1, I2=I2, opts=opts, Mo=Mo, No=No, map=mpg, gate_its=gate_its, map1=mp1, flo=flo, unk=unk, split=split, seed=rank,
                 kernel=f"gq::k_iter<{R},float,{ksuf},Q> (VV stored as float: integer frames)",
                 workload=f"{label}: {name} {No}x{Mo} {engine} L={L} K={K} its={args.steps} "
                          f"(one step = one full-frame iteration)")
+
+
+TRACK_ITS = 60  # iterations of the per-iteration divergence record (parity gate)
+
+
+def literal_engine_leg(args, rank, barrier, opts, I1, I2, flo, unk, gate_its, device):
+    """The literal-order engine (options arith="literal": every expression of
+    gqmap_gpu_mixture.m:87-182 in the reference's own order, k_iter_lit) on
+    the same pair, seed and steps: timed like the headline (settled clocks,
+    gqmap_run graph replay), its k_iter_lit mean from an instrumented replay,
+    and its flow after gate_its iterations for the parity gate (bit-identical
+    to the literal restatement with the same Gauss-Hermite rule)."""
+    from gqmap_opticalflow_amd import Engine, aepe
+    eng = Engine(dict(opts, arith="literal"), I1, I2, "mixture", "fp64", device=device)
+    try:
+        eng.init_state(seed=rank)
+        if args.warmup:
+            eng.run(args.warmup)
+        eng.prepare()
+
+        def chunk():
+            eng.init_state(seed=rank)
+            eng.run(20)
+        if not args.no_settle:
+            settle_clocks(chunk, 20)
+        eng.init_state(seed=rank)
+        barrier()
+        t0 = time.perf_counter()
+        done, _ = eng.run(args.steps)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        mp = eng.map()
+        eng.init_state(seed=rank)
+        done2, total_ms, kernel_ms = eng.run_timed(args.steps)
+        replay_same = done2 == done and np.array_equal(eng.map(), mp)
+        mpg = mp
+        if gate_its != args.steps:
+            eng.init_state(seed=rank)
+            eng.run(gate_its)
+            mpg = eng.map()
+        Mo, No = I1.shape
+        return {"value": Mo * No * done / elapsed / 1e9, "unit": "Gpixel-iter/s", "its": done,
+                "ms_per_step": elapsed / max(done, 1) * 1e3, "k_iter_us": kernel_ms / max(done, 1) * 1e3,
+                "instrumented_replay_bit_exact": bool(replay_same), "aepe_gpu": aepe(flo, mp, unk),
+                "kernel": "gq::k_iter_lit<float,false> (literal order, fp64 arithmetic, VV stored as float)",
+                "map": mpg}
+    finally:
+        eng.close()
 
 
 def run_c3(args, rank, world, local, barrier):
@@ -527,7 +670,50 @@ def parity_gate_c1(r, steps):
                     "restatement's operation order, so the flows are bit-identical"}
 
 
-def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts):
+STRIP_PLANES = ("muu", "muv", "sigu", "sigv", "pn", "rou")
+
+
+def gather_strips(dist, world, owned, col0, col1):
+    """Every rank's owned node columns [col0, col1) of the state planes
+    (STRIP_PLANES order) to rank 0: a list of (col0, col1, planes) in rank
+    order there, None on the other ranks."""
+    mine = (int(col0), int(col1), [np.array(p, order="F", copy=True) for p in owned])
+    if dist is None or world == 1:
+        return [mine]
+    rank = dist.get_rank()
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object(mine, parts, dst=0)
+    return parts
+
+
+def strip_parity(parts, whole, strip_trace=None, whole_trace=None, strip_done=None, whole_done=None):
+    """The strips assembled into the full grid against a whole-grid solve of
+    the same pair, seed and lanes per node (a Jacobi update with exact totals:
+    they must agree bit for bit, gqmap_gpu_mixture.m:29-46).  whole: the
+    full-grid planes in STRIP_PLANES order.  Returns the record the line
+    carries (bit_exact, per-plane mismatching values, uncovered columns, the
+    stop iteration of both, the trace comparison)."""
+    mism = {}
+    cover = np.zeros(whole[0].shape[1], dtype=int)
+    for c0, c1, _ in parts:
+        cover[c0:c1] += 1
+    for i, name in enumerate(STRIP_PLANES):
+        glob = np.zeros_like(whole[i])
+        for c0, c1, owned in parts:
+            glob[:, c0:c1] = owned[i]
+        mism[name] = int(np.sum(glob != whole[i]))
+    rec = {"bit_exact": all(v == 0 for v in mism.values()) and bool(np.all(cover == 1)),
+           "mismatch": mism, "columns_not_covered_once": int(np.sum(cover != 1))}
+    if strip_done is not None:
+        rec["stop_iteration"] = {"strips": int(strip_done), "whole": int(whole_done)}
+        rec["bit_exact"] = rec["bit_exact"] and strip_done == whole_done
+    if strip_trace is not None:
+        rec["trace_bit_exact"] = bool(np.array_equal(strip_trace, whole_trace))
+        rec["bit_exact"] = rec["bit_exact"] and rec["trace_bit_exact"]
+    return rec
+
+
+def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts, validate=True):
     """One frame as column-strip tiles over the ranks (gqmap_create_tile):
     RCCL ghost-column and exact-totals exchange every iteration.  Returns the
     rank's timing and its share of the AEPE sums (interior pixels)."""
@@ -556,7 +742,7 @@ def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
         eng.init_state(seed=0)  # timed steps are iterations 1..steps of the solve
         barrier()
         t0 = time.perf_counter()
-        done, _ = eng.run(args.steps)  # production path: graph replay
+        done, tr = eng.run(args.steps)  # production path: graph replay
         barrier()
         elapsed = time.perf_counter() - t0
         if done != args.steps:
@@ -569,6 +755,21 @@ def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
         done2, total_ms, kernel_ms = eng.run_timed(args.steps)
         if done2 != args.steps or not np.array_equal(eng.map(), mp):
             raise RuntimeError(f"rank {rank}: the instrumented replay differs from the timed run")
+        sp = None
+        if validate:
+            # the strips' final state (the replay ends where the timed run
+            # did: checked above) against a whole-grid solve on rank 0
+            st = eng.get_state()
+            parts = gather_strips(dist, world, [getattr(st, k)[:, col0:col1] for k in STRIP_PLANES], col0, col1)
+            if rank == 0:
+                with Engine(opts, I1, I2, "mixture", args.precision, device=local) as whole:
+                    whole.init_state(seed=0)
+                    wdone, wtr = whole.run(args.steps)
+                    ws = whole.get_state()
+                sp = strip_parity(parts, [getattr(ws, k) for k in STRIP_PLANES], tr, wtr, done, wdone)
+                sp["reference"] = (f"whole-grid gqmap_run of the same pair, seed and lanes per node (split "
+                                   f"{opts['split']}), {args.steps} iterations")
+            barrier()
     finally:
         eng.close()
     Mo, No = I1.shape
@@ -578,7 +779,7 @@ def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
     f[unk] = 0
     e = np.sqrt(((flo[sl] - f[sl]) ** 2).sum(axis=2))
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, pixels=Mo * No, nodes=Mo * (col1 - col0), settle=settle,
-                err_sum=float(e.sum()), err_n=int(e.size), split=opts["split"])
+                err_sum=float(e.sum()), err_n=int(e.size), split=opts["split"], strip_parity=sp)
 
 
 def run_tiled(args, rank, world, local, barrier, dist, names, scale, label):
@@ -593,7 +794,11 @@ def run_tiled(args, rank, world, local, barrier, dist, names, scale, label):
         _, flo, (minu, maxu, minv, maxv), unk = flow_to_color(gt, device=local)
         opts = dict(its=args.steps, K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdas=5.0, lambdad=1.0,
                     minu=minu, maxu=maxu, minv=minv, maxv=maxv)
-        r = tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts)
+        # the strips are checked against the whole grid on the first pair
+        # (C5's 3.6 Mpx pairs: one whole-grid solve bounds the extra time)
+        r = tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts, validate=not per_pair)
+        if r["strip_parity"] is not None:
+            tot["strip_parity"] = dict(r["strip_parity"], pair=name)
         Mo, No = I1.shape
         for k in ("elapsed", "kernel_ms", "pixels", "nodes"):
             tot[k] += r[k]
@@ -633,6 +838,9 @@ def main():
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the parity gate (CPU model + literal restatement of the same steps, AEPE and "
                          "colour deltas) after the timed region")
+    ap.add_argument("--no-literal", action="store_true",
+                    help="c2/c4 mixture fp64: skip the literal-order engine leg (arith=literal, timed and checked "
+                         "bit for bit against the literal restatement)")
     ap.add_argument("--tiled", action="store_true",
                     help="c2: strong scaling -- the RubberWhale pair split into column strips over the ranks")
     args = ap.parse_args()
@@ -771,6 +979,8 @@ def main():
         if tiled:
             out["per_pair"] = [{k: p[k] for k in ("name", "size", "aepe", "elapsed")} for p in r["per_pair"]]
             out["config"]["split"] = r["split"]
+            if r.get("strip_parity"):
+                out["strip_parity"] = r["strip_parity"]
 
     printed = []
 
@@ -810,6 +1020,11 @@ def main():
                     "workload": f"rubberwhale {pp['size']} mixture L=1 K=9 its={args.steps}, one column strip per "
                                 f"rank, Q={st['split']} lanes per node (from one strip)",
                     "aepe": None}
+                spr = st.get("strip_parity")
+                if spr:
+                    out["strong_scaling"]["bit_exact"] = spr["bit_exact"]
+                    out["strong_scaling"]["stop_iteration"] = spr.get("stop_iteration")
+                    out["strong_scaling"]["strip_parity"] = spr
         except Exception as e:  # reported in the line; the frame-parallel value stands
             if out is not None:
                 out["strong_scaling"] = {"error": f"{type(e).__name__}: {e}"[:300]}
@@ -827,8 +1042,15 @@ def main():
         try:
             par = parity_gate(r, engine, r["gate_its"], args.precision, r["split"], r["seed"])
             out["parity"] = par
-            for k in ("aepe_cpu_emul", "aepe_cpu_literal", "aepe_delta_emul", "aepe_delta_literal"):
-                out[k] = par[k]
+            for k in ("aepe_cpu_emul", "aepe_cpu_literal", "aepe_delta_emul", "aepe_delta_literal",
+                      "aepe_spread_literal"):
+                if k in par:
+                    out[k] = par[k]
+            if r.get("literal") is not None:
+                le = {k: v for k, v in r["literal"].items() if k != "map"}
+                le.update(par.get("literal_engine", {}))
+                out["literal_engine"] = le
+                par.pop("literal_engine", None)
             out["colour_mismatch"] = par["colour_mismatch_emul"]
             out["colour_mismatch_literal"] = par["colour_mismatch_literal"]
         except Exception as e:  # reported, never hides the measured line
@@ -848,6 +1070,13 @@ def main():
     emit()
     if dist is not None:
         dist.destroy_process_group()
+    # a tiled solve that is not bit-identical to the whole grid fails the run
+    # (after the line is out)
+    if out is not None:
+        for rec in (out.get("strip_parity"), (out.get("strong_scaling") or {}).get("strip_parity")):
+            if rec is not None and not rec["bit_exact"]:
+                print("bench: column strips differ from the whole-grid solve", file=sys.stderr)
+                sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -18,6 +18,8 @@ GQMAP_OK = 0
 ENGINE_MIXTURE, ENGINE_SUPER, ENGINE_CTF = 0, 1, 2
 FP64, FP32 = 0, 1
 ALPHA_SOFTMAX, ALPHA_PROJSPLX = 0, 1
+ARITH_FAST, ARITH_LITERAL = 0, 1  # gqmap_options.arith (ABI 2)
+ABI_VERSION = 2
 SPLIT_ROLE = -1  # GQMAP_SPLIT_ROLE: options["split"] for the role-split kernel shape (Q = 1 arithmetic)
 LMAX, KMAX = 8, 16
 
@@ -49,6 +51,7 @@ class GqmapOptions(C.Structure):
         ("step0", C.c_double), ("step_decay", C.c_double),
         ("sig_lo", C.c_double), ("sig_hi", C.c_double), ("corr_tor", C.c_double),
         ("tor", C.c_double), ("split", C.c_int), ("sig_step", C.c_double), ("sig_init", C.c_double),
+        ("arith", C.c_int),
     ]
 
 
@@ -89,6 +92,10 @@ def load():
         raise GqmapError(f"{LIB_PATH} not built: run `make -C {PKG_DIR}` "
                          "(or __graft_entry__.build())")
     lib = C.CDLL(LIB_PATH)
+    lib.gqmap_abi_version.restype = C.c_int
+    if lib.gqmap_abi_version() != ABI_VERSION:
+        raise GqmapError(f"{LIB_PATH}: ABI {lib.gqmap_abi_version()}, this binding is ABI {ABI_VERSION} "
+                         "(rebuild the library)")
     P = C.POINTER
     u8 = P(C.c_uint8)
     vp = C.c_void_p

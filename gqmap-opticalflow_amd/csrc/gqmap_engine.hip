@@ -809,11 +809,16 @@ __device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, 
 // the other buffer, and the tile's exact partial sums into partial row part_r.
 // Tcur: the temperature of this iteration (Ctl::T; the persistent kernel keeps
 // its own copy).  tab_ready: the LDS table is already loaded (persistent).
-template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false, bool NT = false>
+// LIT: the literal-order arithmetic of gqmap_math.h (lit_node_grad /
+// lit_edge_grad; fp64 single-scale mixture engine, Q = 1) in place of the fast
+// specification's node_sums / edge_sums; everything around it is shared.
+template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = false, bool NT = false,
+          bool LIT = false>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
                                           int part_r, TileLdsQ<R, Q> &lds, int l0, int l1, double Tcur,
                                           bool tab_ready)
 {
+    static_assert(!LIT || (ENG == 0 && Q == 1 && sizeof(R) == 8), "literal order: fp64 mixture, Q = 1");
     constexpr bool RS = Q == 0;                       // role split (node / edge waves)
     constexpr int QA = arith_q(Q);                    // lanes per node of the arithmetic
     constexpr int TPIX = tile_pix(Q);                 // nodes per tile
@@ -888,7 +893,12 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 #pragma unroll
         for (int ph = 0; ph < 2; ++ph) {
         if ((ph == 0) != EDGE_FIRST) {
-        if (do_node) {
+        if (do_node && LIT) {
+            if constexpr (LIT)
+                if (inner)
+                    nd = lit_node_grad(tab, K2, P.VV, P.M2, P.I1, P.Mo, P.No, P.epsn, P.lamd, P.guard != 0, T, a,
+                                       mu_u, mu_v, sg_u, sg_v, pn, m, n + P.n_off);
+        } else if (do_node) {
         NodeCoef<R> c{};
         if (inner) c = node_coef(sg_u, sg_v, pn);
         // single-scale engine: when no sample of any node of the wave can be
@@ -951,10 +961,14 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
             const bool own_edge = e < 4;
             Grad<R> g{};
             if (jb.need) {
-                const EdgeCoef<R> c = edge_coef(jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
-                Sums<R> S = edge_sums_dev(tab, kj, K2, QA, P.epsn, c);
-                if (QA > 1) S = lane_combine<QA>(S);
-                g = edge_epi(S, c, P.lams, P.guard != 0, T, a, jb.o1, jb.o2, jb.p, ENG == 2);
+                if constexpr (LIT) {
+                    g = lit_edge_grad(tab, K2, P.epsn, P.lams, P.guard != 0, T, a, jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
+                } else {
+                    const EdgeCoef<R> c = edge_coef(jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
+                    Sums<R> S = edge_sums_dev(tab, kj, K2, QA, P.epsn, c);
+                    if (QA > 1) S = lane_combine<QA>(S);
+                    g = edge_epi(S, c, P.lams, P.guard != 0, T, a, jb.o1, jb.o2, jb.p, ENG == 2);
+                }
                 // the edge owns its correlation: clamped ascent right here
                 // (gqmap_gpu_mixture.m:46), nothing else reads drou
                 if (own_edge && inner && lead)
@@ -1029,8 +1043,8 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
 }
 
 
-template <typename R, typename VT, int ENG, int Q, bool NT = false>
-__global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
+template <typename R, typename VT, int ENG, int Q, bool NT = false, bool LIT = false>
+__device__ __forceinline__ void k_iter_body(const IterParams<R, VT> &P)
 {
     Ctl *ctl = P.ctl;
     if (ctl->stop) return;
@@ -1060,13 +1074,13 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
     if (idle) {
         // nothing to compute or add; still takes its arrival ticket below
     } else if (edge_first)
-        iter_tile<R, VT, ENG, Q, true, false, NT>(P, tile, P.spec ? ctl->it_i : ctl->it,
-                                                  (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
-                                                  P.spec ? ctl->T_i : ctl->T, false);
+        iter_tile<R, VT, ENG, Q, true, false, NT, LIT>(P, tile, P.spec ? ctl->it_i : ctl->it,
+                                                       (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
+                                                       P.spec ? ctl->T_i : ctl->T, false);
     else
-        iter_tile<R, VT, ENG, Q, false, false, NT>(P, tile, P.spec ? ctl->it_i : ctl->it,
-                                                   (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
-                                                   P.spec ? ctl->T_i : ctl->T, false);
+        iter_tile<R, VT, ENG, Q, false, false, NT, LIT>(P, tile, P.spec ? ctl->it_i : ctl->it,
+                                                        (P.spec ? ctl->done_i : ctl->done) & 1, part_r, lds, l0, l1,
+                                                        P.spec ? ctl->T_i : ctl->T, false);
 #if GQ_TIMELINE
     __syncthreads();
     TL_STAMP(0, tl0);
@@ -1112,6 +1126,20 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
         if (tl_on) tl_row[7] = __builtin_amdgcn_s_memrealtime();
 #endif
     }
+}
+
+template <typename R, typename VT, int ENG, int Q, bool NT = false>
+__global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R, VT> P)
+{
+    k_iter_body<R, VT, ENG, Q, NT>(P);
+}
+
+// The literal-order arithmetic (gqmap_options.arith = GQMAP_ARITH_LITERAL):
+// the same tiles, halo, update and finalize with lit_node_grad / lit_edge_grad.
+template <typename VT, bool NT = false>
+__global__ __launch_bounds__(BLOCK, 1) void k_iter_lit(IterParams<double, VT> P)
+{
+    k_iter_body<double, VT, 0, 1, NT, true>(P);
 }
 
 
@@ -1766,6 +1794,7 @@ struct gqmap_ctx {
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
+    bool lit = false;   // GQMAP_ARITH_LITERAL: k_iter_lit, literal table layout
     int split = 1;      // lanes per node of the arithmetic (Q): 1, 2, 4, 8, 16, 64
     int kq = 1;         // kernel shape: split, or 0 = role split (Q = 1 arithmetic, 16 x 8 tiles)
     int lpar = 1;       // k_iter blocks per tile (components spread over blocks)
@@ -1881,7 +1910,7 @@ void tile_grid(gqmap_ctx *c)
 {
     // from the whole grid (Ng columns), so every column-strip tile sums its
     // quadrature in the same order as the untiled solve
-    c->split = choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
+    c->split = c->lit ? 1 : choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
     c->kq = c->split;
     if (c->opt.split == GQMAP_SPLIT_ROLE && !c->super_) {  // role split: Q = 1 arithmetic
         c->split = 1;
@@ -2083,6 +2112,17 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
     }
     // (whole grid, one block per tile; lpar_xcd interleaves components instead)
     if (!sg && !P.lpar_xcd) P.band_rows = band_rows(c) ? 1 : 0;
+    if constexpr (Q == 1 && ENG == 0 && sizeof(R) == 8) {
+        if (c->lit) {  // literal-order arithmetic (one instantiation per VV storage and store kind)
+            static const int2 lshape = kernel_shape(k_iter_lit<VT>);
+            if (P.cu_group > 1) P.cu_group = lshape.x;
+            if (state_nt(c))
+                k_iter_lit<VT, true><<<nblocks, BLOCK, 0, c->stream>>>(P);
+            else
+                k_iter_lit<VT><<<nblocks, BLOCK, 0, c->stream>>>(P);
+            return;
+        }
+    }
     if constexpr (Q == 1 && ENG != 1) {
         if (state_nt(c)) {  // frames beyond the L2s: non-temporal state stores
             k_iter<R, VT, ENG, 1, true><<<nblocks, BLOCK, 0, c->stream>>>(P);
@@ -2936,6 +2976,12 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
              "unknown precision %d", opt->precision);
     GQ_CHECK(opt->minu <= opt->maxu && opt->minv <= opt->maxv, GQMAP_ERR_INVALID_ARG,
              "empty flow range");
+    GQ_CHECK(opt->arith == GQMAP_ARITH_FAST || opt->arith == GQMAP_ARITH_LITERAL, GQMAP_ERR_INVALID_ARG,
+             "unknown arith %d", opt->arith);
+    GQ_CHECK(opt->arith != GQMAP_ARITH_LITERAL ||
+                 (opt->engine == GQMAP_ENGINE_MIXTURE && opt->precision == GQMAP_FP64 &&
+                  (opt->split == 0 || opt->split == 1)),
+             GQMAP_ERR_UNSUPPORTED, "literal-order arithmetic: fp64 mixture engine, split 0 or 1");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         set_error("no HIP device available");
@@ -2952,6 +2998,7 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
     c->L = opt->L;
     c->K = opt->K;
     c->K2 = opt->K * opt->K;
+    c->lit = opt->arith == GQMAP_ARITH_LITERAL;
     // quadrature tables, MATLAB meshgrid order k = r + K*c (gqmap_gpu_mixture.m:8-10)
     double X[GQMAP_KMAX], W[GQMAP_KMAX];
     if (gauss_hermite(c->K, X, W) != 0) {
@@ -2964,6 +3011,10 @@ gqmap_status gqmap_create(gqmap_ctx **out, const gqmap_options *opt, int device)
         for (int r = 0; r < c->K; ++r) {
             const int k = r + c->K * cc;
             const double xi = X[cc], xj = X[r], w = W[cc] * W[r];
+            if (c->lit) {  // the literal layout (gqmap_math.h TL_*)
+                lit_table_point(&c->tab_host[tab_at(0, k)], xi, xj, W[cc], W[r]);
+                continue;
+            }
             c->tab_host[tab_at(T_XI, k)] = xi;
             c->tab_host[tab_at(T_XJ, k)] = xj;
             c->tab_host[tab_at(T_W, k)] = w;

@@ -793,4 +793,189 @@ GQ_HD Grad<R> node_grad(TP tab, int K2, VP VV, IP I1, int M2, int Mo, int No, R 
                     lamd, guard, T, a, o1, o2, p, ENG == 2);
 }
 
+// ---------------------------------------------------------------------------
+// Literal-order arithmetic (gqmap_options.arith = GQMAP_ARITH_LITERAL; fp64,
+// single-scale mixture engine, one lane per node).
+//
+// The fast specification above regroups the reference's arithmetic (basis
+// sums, fma, 1/pi folded into a scale, absolute sample positions, mirror
+// pairs): each gradient differs from the reference's by a rounding or two.
+// This variant evaluates every expression of node_grad_spectral /
+// edge_grad_spectral / node_pot / edge_pot (gqmap_gpu_mixture.m:87-182) in
+// MATLAB's left-to-right order with no fused operation: products of three
+// as (a*b)*c, the K^2 quadrature points summed one after the other in
+// meshgrid order, XI2mXJ2(k)/sqrtpr divided per point, the six divisions by
+// pi where the reference has them.  With L = 1 and T = 0 (config C2) every
+// operation of an iteration is then a correctly rounded IEEE +, -, *, /,
+// sqrt, floor or min/max on the same operands as oracle/gqmap_oracle.c
+// (compiled -ffp-contract=off), so the two agree bit for bit at any
+// iteration count (tests/test_emulator.py, tests/test_gpu_literal.py) given
+// the same Gauss-Hermite rule.  (T != 0 adds the entropy log, here the
+// deterministic gq_log instead of libm's log.)  The exact fixed-point pixel
+// sums (Energy, ptdmu) are not part of the state update; they are the
+// correctly rounded sums of the reference's summands.
+//
+// Table rows of a quadrature point in this mode (the 8-entry point-major
+// layout of tab_at): XI, XJ, WIWJ, XI2aXJ2, XI2mXJ2, 2*XIXJ (exact
+// doubling), XI2aXJ2 - 1 (the reference's per-point value: same rounding
+// whether it is formed here or in the loop), unused.
+// ---------------------------------------------------------------------------
+constexpr int TL_XI = 0, TL_XJ = 1, TL_W = 2, TL_A = 3, TL_M = 4, TL_X2 = 5, TL_A1 = 6;
+
+// gqmap_gpu_mixture.m:8-10 (meshgrid: XI(r,c) = X(c), XJ(r,c) = X(r)) for one
+// point k = r + K c: row8 receives the 8 table entries above.  (Host code:
+// gqmap_create builds the table.)
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+inline void lit_table_point(double *row8, double xi, double xj, double wi, double wj)
+{
+    const double a = xi * xi + xj * xj;
+    row8[TL_XI] = xi;
+    row8[TL_XJ] = xj;
+    row8[TL_W] = wi * wj;
+    row8[TL_A] = a;
+    row8[TL_M] = xi * xi - xj * xj;
+    row8[TL_X2] = 2 * (xi * xj);
+    row8[TL_A1] = a - 1;
+    row8[7] = 0;
+}
+
+// node_pot's interpolation (gqmap_gpu_mixture.m:157-176) in its own order:
+// Xq, Yq clamped to [1, N] x [1, M], the cell chosen by the reference's
+// if-chain, each tap weighted as (VV * ss) * tw, the taps added left to right
+// (first column parenthesised as the reference writes it), then /4.
+template <typename VP>
+GQ_HD double lit_interp(VP VV, int M2, int Mo, int No, double Xq, double Yq)
+{
+    Xq = fmin(fmax(Xq, 1.0), (double)No);
+    Yq = fmin(fmax(Yq, 1.0), (double)Mo);
+    int ix, iy;
+    if (Xq <= 1.0) ix = 1;
+    else if (Xq <= No - 1) ix = (int)floor(Xq);
+    else ix = No - 1;
+    if (Yq <= 1.0) iy = 1;
+    else if (Yq <= Mo - 1) iy = (int)floor(Yq);
+    else iy = Mo - 1;
+    const double so = Xq - ix, to = Yq - iy;
+    const double t0 = ((2.0 - to) * to - 1.0) * to;
+    const double t1 = (3.0 * to - 5.0) * to * to + 2.0;
+    const double t2 = ((4.0 - 3.0 * to) * to + 1.0) * to;
+    const double t3 = (to - 1.0) * to * to;
+    const auto c1 = elem_ptr(VV, cell_elem(iy, ix, M2));
+    const auto c2 = elem_ptr(VV, cell_elem(iy, ix + 1, M2));
+    const auto c3 = elem_ptr(VV, cell_elem(iy, ix + 2, M2));
+    const auto c4 = elem_ptr(VV, cell_elem(iy, ix + 3, M2));
+    double ss = ((2.0 - so) * so - 1.0) * so;
+    double Vq = (((double)c1[0] * ss * t0 + (double)c1[1] * ss * t1) + (double)c1[2] * ss * t2) +
+                (double)c1[3] * ss * t3;
+    ss = (3.0 * so - 5.0) * so * so + 2.0;
+    Vq = Vq + (double)c2[0] * ss * t0 + (double)c2[1] * ss * t1 + (double)c2[2] * ss * t2 + (double)c2[3] * ss * t3;
+    ss = ((4.0 - 3.0 * so) * so + 1.0) * so;
+    Vq = Vq + (double)c3[0] * ss * t0 + (double)c3[1] * ss * t1 + (double)c3[2] * ss * t2 + (double)c3[3] * ss * t3;
+    ss = (so - 1.0) * so * so;
+    Vq = Vq + (double)c4[0] * ss * t0 + (double)c4[1] * ss * t1 + (double)c4[2] * ss * t2 + (double)c4[3] * ss * t3;
+    return Vq / 4;
+}
+
+// The six accumulators of the quadrature loop (gqmap_gpu_mixture.m:98-105)
+struct LitAcc {
+    double dp = 0, du1 = 0, du2 = 0, do1 = 0, do2 = 0, Ei = 0;
+    template <typename TP>
+    GQ_HD void add(TP tab, int k, double fval, double zi, double zj, double p, double sqrtpr, bool live)
+    {
+        if (live) {  // `if a~=0` (:98)
+            dp = dp + fval * ((p - p * tab[tab_at(TL_A, k)]) + tab[tab_at(TL_X2, k)]);
+            du1 = du1 + fval * (zi - p * zj);
+            du2 = du2 + fval * (zj - p * zi);
+            const double q = tab[tab_at(TL_M, k)] / sqrtpr;
+            do1 = do1 + fval * (tab[tab_at(TL_A1, k)] + q);
+            do2 = do2 + fval * (tab[tab_at(TL_A1, k)] - q);
+        }
+        Ei = Ei + fval;
+    }
+};
+
+// Spectral coordinates shared by both gradients (:90-93, :120-123)
+struct LitCoef {
+    double s, t, pr, sqrtpr;
+};
+GQ_HD LitCoef lit_coef(double p)
+{
+    LitCoef c;
+    const double sp = GQ_SQRT(1 + p), sm = GQ_SQRT(1 - p);
+    c.s = (sp + sm) / 2;
+    c.t = (sp - sm) / 2;
+    c.pr = 1 - p * p;
+    c.sqrtpr = GQ_SQRT(c.pr);
+    return c;
+}
+
+// Epilogues: node (:107-115, entropy -3T) and edge (:137-145, entropy +T).
+GQ_HD Grad<double> lit_epi(const LitAcc &S, const LitCoef &c, double a, double o1, double o2, double p, double T,
+                           bool node)
+{
+    const double o1pr = GQ_M_SQRT2 / (o1 * c.pr), o2pr = GQ_M_SQRT2 / (o2 * c.pr);
+    Grad<double> g;
+    g.du1 = a * S.du1 * o1pr / GQ_M_PI;
+    g.du2 = a * S.du2 * o2pr / GQ_M_PI;
+    // T (const1 + log(.)): a finite value times 0 when T = 0 -- skipped then
+    // (the difference Ei/pi -+ 0 is Ei/pi: Ei < 0 never vanishes)
+    const double ent = T != 0 ? (1 + gq_log(2 * GQ_M_PI)) + gq_log(c.sqrtpr * o1 * o2) : 0.0;
+    if (node) {
+        g.da = S.Ei / GQ_M_PI - 3 * T * ent;
+        g.do1 = a * (S.do1 / GQ_M_PI - 3 * T) / o1;
+        g.do2 = a * (S.do2 / GQ_M_PI - 3 * T) / o2;
+        g.dp = a * (S.dp / GQ_M_PI + 3 * T * p) / c.pr;
+    } else {
+        g.da = S.Ei / GQ_M_PI + T * ent;
+        g.do1 = a * (S.do1 / GQ_M_PI + T) / o1;
+        g.do2 = a * (S.do2 / GQ_M_PI + T) / o2;
+        g.dp = a * (S.dp / GQ_M_PI - T * p) / c.pr;
+    }
+    g.E = a * g.da;
+    return g;
+}
+
+// node_grad_spectral with node_pot, (m, n) 0-based pixel of the frame
+template <typename TP, typename VP, typename IP>
+GQ_HD Grad<double> lit_node_grad(TP tab, int K2, VP VV, int M2, IP I1, int Mo, int No, double eps, double lamd,
+                                 bool guard, double T, double a, double u1, double u2, double o1, double o2, double p,
+                                 int m, int n)
+{
+    const LitCoef c = lit_coef(p);
+    const double so1 = GQ_M_SQRT2 * o1, so2 = GQ_M_SQRT2 * o2;
+    const double I = I1[m + (int64_t)Mo * n];
+    const bool live = !guard || a != 0;
+    LitAcc S;
+    for (int k = 0; k < K2; ++k) {
+        const double XI = tab[tab_at(TL_XI, k)], XJ = tab[tab_at(TL_XJ, k)];
+        const double zi = c.s * XI + c.t * XJ, zj = c.t * XI + c.s * XJ;
+        const double x1 = so1 * zi + u1, x2 = so2 * zj + u2;
+        const double d = I - lit_interp(VV, M2, Mo, No, (double)(n + 1) + x1, (double)(m + 1) + x2);
+        const double fval = tab[tab_at(TL_W, k)] * (-lamd * GQ_SQRT(eps + d * d));
+        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, live);
+    }
+    return lit_epi(S, c, a, o1, o2, p, T, true);
+}
+
+// edge_grad_spectral with edge_pot
+template <typename TP>
+GQ_HD Grad<double> lit_edge_grad(TP tab, int K2, double eps, double lams, bool guard, double T, double a, double u1,
+                                 double u2, double o1, double o2, double p)
+{
+    const LitCoef c = lit_coef(p);
+    const double so1 = GQ_M_SQRT2 * o1, so2 = GQ_M_SQRT2 * o2;
+    const bool live = !guard || a != 0;
+    LitAcc S;
+    for (int k = 0; k < K2; ++k) {
+        const double XI = tab[tab_at(TL_XI, k)], XJ = tab[tab_at(TL_XJ, k)];
+        const double zi = c.s * XI + c.t * XJ, zj = c.t * XI + c.s * XJ;
+        const double d = (so1 * zi + u1) - (so2 * zj + u2);
+        const double fval = tab[tab_at(TL_W, k)] * (-lams * GQ_SQRT(eps + d * d));
+        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, live);
+    }
+    return lit_epi(S, c, a, o1, o2, p, T, false);
+}
+
 }  // namespace gq

@@ -27,7 +27,8 @@ from .ops import flow_to_color
 ENGINES = {"mixture": _lib.ENGINE_MIXTURE, "super": _lib.ENGINE_SUPER, "ctf": _lib.ENGINE_CTF}
 PRECISIONS = {"fp64": _lib.FP64, "fp32": _lib.FP32}
 KNOBS = ("alpha_mode", "alpha_start", "alpha_lr", "guard_a", "t_decay_every", "t_min", "step0",
-         "step_decay", "sig_lo", "sig_hi", "corr_tor", "tor", "split", "sig_step", "sig_init")
+         "step_decay", "sig_lo", "sig_hi", "corr_tor", "tor", "split", "sig_step", "sig_init", "arith")
+ARITH = {"fast": _lib.ARITH_FAST, "literal": _lib.ARITH_LITERAL}
 
 
 def make_options(options: dict, engine: str = "mixture", precision: str = "fp64") -> _lib.GqmapOptions:
@@ -46,7 +47,10 @@ def make_options(options: dict, engine: str = "mixture", precision: str = "fp64"
     for k in KNOBS:
         if k in options:
             cur = getattr(o, k)
-            setattr(o, k, type(cur)(options[k]))
+            v = options[k]
+            if k == "arith" and isinstance(v, str):
+                v = ARITH[v]
+            setattr(o, k, type(cur)(v))
     o.engine = ENGINES[engine]
     o.precision = PRECISIONS[precision]
     return o

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GQMAP_ABI_VERSION 1
+#define GQMAP_ABI_VERSION 2  /* 2: gqmap_options.arith */
 #define GQMAP_LMAX 8   /* mixture components supported (reference uses L<=3) */
 #define GQMAP_KMAX 16  /* quadrature order supported (reference uses K=9, 11) */
 
@@ -55,6 +55,17 @@ typedef enum gqmap_engine_kind {
 typedef enum gqmap_precision { GQMAP_FP64 = 0, GQMAP_FP32 = 1 } gqmap_precision;
 /* gqmap_options.split: Q = 1 arithmetic, node and edge phases on separate waves */
 #define GQMAP_SPLIT_ROLE (-1)
+/* gqmap_options.arith: the order of the per-node arithmetic.
+ *  FAST    the kernel's specification (gqmap_math.h: basis sums, fma, 1/pi
+ *          folded into a scale) -- within a rounding or two per gradient of
+ *          the reference's expressions, the fastest form.
+ *  LITERAL every expression of node_grad_spectral / edge_grad_spectral /
+ *          node_pot / edge_pot (gqmap_gpu_mixture.m:87-182) in the
+ *          reference's own order, no fused operations: bit-identical to the
+ *          literal restatement oracle/gqmap_oracle.c while the alpha update
+ *          is off (L = 1, or it <= alpha_start).  fp64 mixture engine only,
+ *          one lane per node (split 0 or 1). */
+typedef enum gqmap_arith { GQMAP_ARITH_FAST = 0, GQMAP_ARITH_LITERAL = 1 } gqmap_arith;
 typedef enum gqmap_alpha_mode {
     GQMAP_ALPHA_SOFTMAX = 0,   /* updateAlpha, gqmap_gpu_mixture.m:78-86 (live path)   */
     GQMAP_ALPHA_PROJSPLX = 1   /* projsplx(alpha+dalpha*step*lr), :49 (commented out)   */
@@ -88,6 +99,7 @@ typedef struct gqmap_options {
                             edge phases on separate waves (mid-size grids)       */
     double sig_step;     /* sigma step scale: 1, ctf 0.3 (gqmap_ctf.m:34-35)     */
     double sig_init;     /* init sigma = U + sig_init; < 0: U + (max - min)      */
+    int arith;           /* gqmap_arith (ABI 2)                                  */
 } gqmap_options;
 
 /* Engine state, MATLAB layout (M x N x L [x 2 x 2]).  M,N = node grid

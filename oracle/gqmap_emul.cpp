@@ -76,7 +76,8 @@ auto split_sums(int Q, F part) -> decltype(part(0, 1))
     return butterfly(parts, Q);
 }
 
-template <typename R, int ENG>
+// LIT: the literal-order arithmetic of gqmap_math.h (lit_*; fp64 mixture, Q = 1)
+template <typename R, int ENG, bool LIT = false>
 int run_t(const orc_params *P, const double *X, const double *W, const double *I1,
           const double *VV, orc_state *S, double *T_io, int it_first, int n_iter, double *trace,
           int Q, const Geo &G, int64_t *totals_out)
@@ -95,6 +96,10 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
         for (int r = 0; r < P->K; ++r) {
             const int k = r + P->K * cc;
             const double xi = X[cc], xj = X[r], ww = W[cc] * W[r];
+            if (LIT) {
+                lit_table_point(&tabd[tab_at(0, k)], xi, xj, W[cc], W[r]);
+                continue;
+            }
             tabd[tab_at(T_XI, k)] = xi;
             tabd[tab_at(T_XJ, k)] = xj;
             tabd[tab_at(T_W, k)] = ww;
@@ -140,7 +145,12 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                 for (int m = 0; m < M; ++m) {
                     const int64_t i = m + (int64_t)M * n + MN * l;
                     const bool inner = G.upd(m, n, M);
-                    if (inner) {
+                    if (inner && LIT) {
+                        if constexpr (LIT)
+                            w.node[i] = lit_node_grad(tab, w.K2, VVp, w.M2, I1p, w.Mo, w.No, eps, lamd, guard, Tr, a,
+                                                      st[i], st[i + MNL], st[i + 2 * MNL], st[i + 3 * MNL],
+                                                      st[i + 4 * MNL], m, n + G.n_off);
+                    } else if (inner) {
                         const NodeCoef<R> c = node_coef(st[i + 2 * MNL], st[i + 3 * MNL], st[i + 4 * MNL]);
                         const Sums<R> Sn = split_sums(Q, [&](int k0, int dk) {
                             return node_sums<ENG>(tab, k0, w.K2, dk, frame_view(VVp, w.M2), I1p, w.Mo, w.No, eps,
@@ -158,6 +168,11 @@ int run_t(const orc_params *P, const double *X, const double *W, const double *I
                             const int64_t r = rm + (int64_t)M * rn + MN * l;
                             const R o1 = st[i + MNL * (2 + uv)], o2 = st[r + MNL * (2 + uv)];
                             const R p = st[i + MNL * (5 + e)];
+                            if constexpr (LIT) {
+                                w.edge[i * 4 + e] = lit_edge_grad(tab, w.K2, eps, lams, guard, Tr, a, st[i + MNL * uv],
+                                                                  st[r + MNL * uv], o1, o2, p);
+                                continue;
+                            }
                             const EdgeCoef<R> c = edge_coef(st[i + MNL * uv], st[r + MNL * uv], o1, o2, p);
                             // Q = 64 (one wave per node): the edges run on 16-lane groups
                             const Sums<R> Se = split_sums(edge_parts(Q), [&](int k0, int dk) {
@@ -334,6 +349,21 @@ extern "C" int emu_run(const orc_params *P, const double *X, const double *W, co
                 : run_eng<double>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, Q, G, nullptr);
 }
 
+/* The literal-order arithmetic (gqmap_options.arith = GQMAP_ARITH_LITERAL):
+ * fp64 single-scale mixture engine, one lane per node; geo as emu_run_tile
+ * (NULL: the whole grid), totals may be NULL.  Returns -2 for another engine. */
+extern "C" int emu_run_lit(const orc_params *P, const double *X, const double *W, const double *I1,
+                           const double *VV, orc_state *S, double *T_io, int it_first, int n_iter,
+                           double *trace, int nthreads, const int *geo, int64_t *totals)
+{
+    if (P->ctf || P->super_) return -2;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    const Geo G = geo ? Geo{geo[0], geo[1], geo[2], geo[3]} : Geo{0, 0, P->N, P->N};
+    return run_t<double, 0, true>(P, X, W, I1, VV, S, T_io, it_first, n_iter, trace, 1, G, totals);
+}
+
 extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)
 {
     for (int64_t i = 0; i < n; ++i)
@@ -343,6 +373,7 @@ extern "C" void emu_math(int fn, const double *in, double *out, int64_t n)
 
 // the device's deterministic exp as a plain function (orc_set_map_exp)
 extern "C" double emu_gq_exp(double x) { return gq_exp(x); }
+extern "C" double emu_gq_log(double x) { return gq_log(x); }
 
 
 

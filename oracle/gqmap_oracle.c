@@ -149,7 +149,12 @@ static void ctx_init(orc_ctx *c, const orc_params *p, const double *I1, const do
 {
     double X[KMAX], W[KMAX];
     c->p = p; c->I1 = I1; c->VV = VV;
-    orc_gauss_hermite(p->K, X, W);
+    if (p->gh_x && p->gh_w) {
+        memcpy(X, p->gh_x, sizeof(double) * (size_t)p->K);
+        memcpy(W, p->gh_w, sizeof(double) * (size_t)p->K);
+    } else {
+        orc_gauss_hermite(p->K, X, W);
+    }
     c->K2 = p->K * p->K;
     /* [XI,XJ] = meshgrid(X): XI(r,c)=X(c), XJ(r,c)=X(r); linear k = r + K*c */
     for (int cc = 0; cc < p->K; ++cc)
@@ -255,6 +260,13 @@ static inline double edge_pot(const orc_ctx *c, double x1, double x2)
     return -c->p->lambdas * sqrt(c->p->epsn + d * d);
 }
 
+/* log of the entropy terms (:111, :141): libm by default; orc_set_ent_log()
+ * swaps in another implementation (the device's deterministic gq_log, from
+ * the emulator) so that T != 0 runs can be compared bit for bit with the
+ * literal-order engine.  MATLAB's own log is unpinned. */
+static double (*ent_log)(double) = log;
+void orc_set_ent_log(double (*f)(double)) { ent_log = f ? f : log; }
+
 /* node_grad_spectral: gqmap_gpu_mixture.m:87-116 (super: gqmap_gpuSuper_mix_entropy.m:87-122).
  * m, n are 1-based node indices.  out = {da,du1,du2,do1,do2,dp,Ei}. */
 static void node_grad(const orc_ctx *c, double T, double a, double u1, double u2, double o1,
@@ -266,7 +278,7 @@ static void node_grad(const orc_ctx *c, double T, double a, double u1, double u2
     const double t = (sqrt(1 + p) - sqrt(1 - p)) / 2;
     const double pr = 1 - p * p, sqrtpr = sqrt(pr);
     const double o1pr = SQRT2 / (o1 * pr), o2pr = SQRT2 / (o2 * pr);
-    const double const1 = 1 + log(2 * M_PI);
+    const double const1 = 1 + ent_log(2 * M_PI);
     for (int k = 0; k < c->K2; ++k) {
         const double zi = s * c->XI[k] + t * c->XJ[k], zj = t * c->XI[k] + s * c->XJ[k];
         const double x1 = SQRT2 * o1 * zi + u1, x2 = SQRT2 * o2 * zj + u2;
@@ -292,7 +304,7 @@ static void node_grad(const orc_ctx *c, double T, double a, double u1, double u2
     }
     du1 = a * du1 * o1pr / M_PI;
     du2 = a * du2 * o2pr / M_PI;
-    const double da = Ei / M_PI - 3 * T * (const1 + log(sqrtpr * o1 * o2));
+    const double da = Ei / M_PI - 3 * T * (const1 + ent_log(sqrtpr * o1 * o2));
     do1 = a * (do1 / M_PI - 3 * T) / o1;
     do2 = a * (do2 / M_PI - 3 * T) / o2;
     dp = a * (dp / M_PI + 3 * T * p) / pr;
@@ -310,7 +322,7 @@ static void edge_grad(const orc_ctx *c, double T, double a, double u1, double u2
     const double t = (sqrt(1 + p) - sqrt(1 - p)) / 2;
     const double pr = 1 - p * p, sqrtpr = sqrt(pr);
     const double o1pr = SQRT2 / (o1 * pr), o2pr = SQRT2 / (o2 * pr);
-    const double const1 = 1 + log(2 * M_PI);
+    const double const1 = 1 + ent_log(2 * M_PI);
     for (int k = 0; k < c->K2; ++k) {
         const double zi = s * c->XI[k] + t * c->XJ[k], zj = t * c->XI[k] + s * c->XJ[k];
         const double x1 = SQRT2 * o1 * zi + u1, x2 = SQRT2 * o2 * zj + u2;
@@ -326,7 +338,7 @@ static void edge_grad(const orc_ctx *c, double T, double a, double u1, double u2
     }
     du1 = a * du1 * o1pr / M_PI;
     du2 = a * du2 * o2pr / M_PI;
-    const double da = Ei / M_PI + T * (const1 + log(sqrtpr * o1 * o2));
+    const double da = Ei / M_PI + T * (const1 + ent_log(sqrtpr * o1 * o2));
     do1 = a * (do1 / M_PI + T) / o1;
     do2 = a * (do2 / M_PI + T) / o2;
     dp = a * (dp / M_PI - T * p) / pr;

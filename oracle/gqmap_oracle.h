@@ -39,6 +39,11 @@ typedef struct {
     double tor;          /* stop when ptdmu < tor (:75)                        */
     int ctf;             /* 1: legacy/gqmap_ctf.m level solver (rounded I2_cont lookup) */
     double sig_step;     /* sigma step scale (ctf: 0.3, gqmap_ctf.m:34-35)     */
+    /* Gauss-Hermite rule (K nodes ascending, weights): NULL = this library's
+     * restatement of GaussHermite_2.m (orc_gauss_hermite); otherwise the
+     * caller's rule, so the iteration arithmetic can be compared bit for bit
+     * with an engine that uses another (equally accurate) rule. */
+    const double *gh_x, *gh_w;
 } orc_params;
 
 typedef struct {
@@ -67,6 +72,9 @@ int orc_run(const orc_params *p, const double *I1, const double *VV, orc_state *
 void orc_gradients(const orc_params *p, const double *I1, const double *VV,
                    const orc_state *st, double T, double *node_out, double *edge_out,
                    int nthreads);
+
+/* The log of the entropy terms: NULL = libm log (default), else f. */
+void orc_set_ent_log(double (*f)(double));
 
 /* projsplx.m:15-30 */
 void orc_projsplx(const double *y, double *x, int n);

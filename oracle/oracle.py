@@ -30,6 +30,7 @@ class OrcParams(C.Structure):
         ("sig_lo", C.c_double), ("sig_hi", C.c_double), ("corr_tor", C.c_double),
         ("alpha_mode", C.c_int), ("alpha_start", C.c_int), ("alpha_lr", C.c_double),
         ("tor", C.c_double), ("ctf", C.c_int), ("sig_step", C.c_double),
+        ("gh_x", C.POINTER(C.c_double)), ("gh_w", C.POINTER(C.c_double)),
     ]
 
 
@@ -151,17 +152,32 @@ class State:
 
 
 def run(opts: dict, I1: np.ndarray, I2: np.ndarray, state: State, it_first: int, n_iter: int,
-        T: float | None = None, nthreads: int = 0):
-    """Run n_iter iterations in place on `state`.  Returns (done, trace[done,3], T)."""
+        T: float | None = None, nthreads: int = 0, X=None, W=None, det_log: bool = False):
+    """Run n_iter iterations in place on `state`.  Returns (done, trace[done,3], T).
+    X, W: a Gauss-Hermite rule to use instead of the restated GaussHermite_2.m
+    (orc_gauss_hermite) -- e.g. the product's, to compare the iteration
+    arithmetic bit for bit with the literal-order engine.  det_log: the
+    entropy terms use the device's deterministic log (gqmap_math.h gq_log)
+    instead of libm's (T != 0 runs compared bit for bit)."""
     I1 = _f64(I1)
     Mo, No = I1.shape
     p = make_params(opts, Mo, No)
+    if X is not None:
+        X, W = _f64(np.asarray(X, dtype=np.float64)), _f64(np.asarray(W, dtype=np.float64))
+        p.gh_x, p.gh_w = _p(X), _p(W)
     VV = get_vv(I2)
     Tbox = (C.c_double * 1)(p.T if T is None else T)
     trace = np.zeros((max(n_iter, 1), 3))
     cs = state.cstruct()
-    done = lib().orc_run(C.byref(p), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
-                         _p(trace), nthreads)
+    L_ = lib()
+    L_.orc_set_ent_log.argtypes = [C.c_void_p]
+    if det_log:
+        L_.orc_set_ent_log(C.cast(L_.emu_gq_log, C.c_void_p))
+    try:
+        done = L_.orc_run(C.byref(p), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
+                          _p(trace), nthreads)
+    finally:
+        L_.orc_set_ent_log(None)
     return done, trace[:done].copy(), Tbox[0]
 
 
@@ -276,6 +292,31 @@ def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
              _p(trace), nthreads, int(fp32), Q)
     if done < 0:
         raise RuntimeError("emu_run failed")
+    return done, trace[:done].copy(), Tbox[0]
+
+
+def emu_run_lit(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
+                T: float | None = None, nthreads: int = 0, geo=None):
+    """CPU model of the literal-order engine (gqmap_options.arith = literal;
+    gqmap_math.h lit_*): fp64 mixture, Q = 1.  geo as emu_run_tile (None: the
+    whole grid).  Returns (done, trace[done,3], T)."""
+    I1 = _f64(I1)
+    Mo, No = I1.shape
+    p = make_params(opts, Mo, No)
+    if geo is not None:
+        p.N = state.muu.shape[1]
+    VV = get_vv(I2)
+    X, W = _f64(np.asarray(X, dtype=np.float64)), _f64(np.asarray(W, dtype=np.float64))
+    Tbox = (C.c_double * 1)(p.T if T is None else T)
+    trace = np.zeros((max(n_iter, 1), 3))
+    g = (C.c_int * 4)(*[int(v) for v in geo]) if geo is not None else None
+    f = lib().emu_run_lit
+    f.restype = C.c_int
+    cs = state.cstruct()
+    done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter, _p(trace),
+             nthreads, g, None)
+    if done < 0:
+        raise RuntimeError("emu_run_lit: literal mode is the fp64 single-scale mixture engine")
     return done, trace[:done].copy(), Tbox[0]
 
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.gqmap_abi_version() == 1
+    assert lib.gqmap_abi_version() == 2
 
 
 def test_header_constants_mirrored():

@@ -150,11 +150,14 @@ def _gloo_worker(rank, world, port, its, result_q):
             tot = [sum(x) for x in zip(*allt)]
             cnt = (M - 2) * (N - 2) * L
             trace.append((oracle.from_fix(tot[0]), oracle.from_fix(tot[1]) / cnt))
-        owned = [a[:, lo:hi].copy() for a in s.arrays()[:6]]
-        gathered = [None] * world
-        dist.all_gather_object(gathered, (col0, col1, owned))
+        # bench.py's strong-scaling check: the strips gathered to rank 0
+        import bench
+        owned = [a[:, lo:hi] for a in s.arrays()[:6]]
+        gathered = bench.gather_strips(dist, world, owned, col0, col1)
         if rank == 0:
             result_q.put((gathered, trace))
+        else:
+            assert gathered is None
     finally:
         dist.destroy_process_group()
 
@@ -178,12 +181,16 @@ def test_tiles_over_gloo_two_ranks(oracle_lib):
         assert p.exitcode == 0
     I1, I2, o, st = _case(3, "mixture")
     ref, tr = _whole(I1, I2, o, st, its)
-    for k_i, (k, a) in enumerate(zip(G.STATE_KEYS[:6], ref.arrays()[:6])):
-        glob = np.zeros_like(a)
-        for col0, col1, owned in gathered:
-            glob[:, col0:col1] = owned[k_i]
-        np.testing.assert_array_equal(glob, a, err_msg=k)
-    np.testing.assert_array_equal(np.array(trace), tr[:, :2])
+    import bench
+    rec = bench.strip_parity(gathered, ref.arrays()[:6], np.array(trace), tr[:, :2], its, len(tr))
+    assert rec["bit_exact"], rec
+    assert rec["columns_not_covered_once"] == 0 and rec["trace_bit_exact"]
+    # the check itself catches a differing strip, a missing column and a different stop
+    bad = [(c0, c1, [a.copy() for a in ow]) for c0, c1, ow in gathered]
+    bad[1][2][0][3, 0, 0] += 1e-15
+    assert bench.strip_parity(bad, ref.arrays()[:6])["mismatch"]["muu"] == 1
+    assert not bench.strip_parity(gathered[:1], ref.arrays()[:6])["bit_exact"]
+    assert not bench.strip_parity(gathered, ref.arrays()[:6], strip_done=its - 1, whole_done=its)["bit_exact"]
 
 
 def test_strip_split_mirrors_library_thresholds():
