@@ -159,6 +159,19 @@ def load():
     return lib
 
 
+def debug_policy(name: str, value: int) -> None:
+    """Set one execution policy of the library (gqmap_debug_policy, not in the
+    public header): placement / caching / launch-shape choices that never
+    change a result -- nt_state, band_rows, cu_group, lpar, lpar_xcd,
+    fused_finalize, persist, persist_cap, graph, vv_float, verbose.  value -1
+    restores the automatic choice.  Contexts created afterwards use it."""
+    f = load().gqmap_debug_policy
+    f.restype = C.c_int
+    f.argtypes = [C.c_char_p, C.c_int]
+    if f(name.encode(), int(value)) != 0:
+        raise GqmapError(f"unknown policy {name!r}")
+
+
 def check(status: int, what: str = "gqmap") -> None:
     if status != GQMAP_OK:
         msg = load().gqmap_last_error().decode(errors="replace")

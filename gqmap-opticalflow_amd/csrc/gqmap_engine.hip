@@ -116,14 +116,17 @@ struct Ctl {
     // them.  One slice per XCD (blocks go round-robin to the 8 XCDs): fewer
     // atomics on one address when a small grid's workgroups end together.
     unsigned long long acc[ACC_SLICES][NFIX + GQMAP_LMAX][4];
-    // speculative RCCL tiles (L = 1): the iteration the kernels run next --
-    // advanced by the ghost unpack, ahead of it / done / T, which the
-    // finalize advances when it has judged the stop rule (launch_step_rccl_spec).
-    // A cache line of their own: the two kernels that write them and it / done
-    // / T may run at the same time on different XCDs.
+    // deferred-totals RCCL tiles (L = 1, launch_seq_deferred): the iteration
+    // the kernels run next -- advanced by the ghost unpack every iteration,
+    // ahead of it / done / T, which the sequence's finalize advances when it
+    // has judged the stop rule on the all-gathered totals.  A cache line of
+    // their own.  ovr: 1 + the sequence row whose totals met the stop rule
+    // when later iterations of the sequence had already run (the host then
+    // restores the sequence's snapshot and re-runs it exactly, deferred_recover).
     alignas(128) int it_i;
     int done_i;
     double T_i;
+    int ovr;
 };
 
 struct FinParams {
@@ -1530,6 +1533,55 @@ __global__ __launch_bounds__(256) void k_finalize(FinParams F)
     if (threadIdx.x == 0) fin_apply(F, tot);
 }
 
+// Deferred-totals RCCL sequence (launch_seq_deferred): the state buffer the
+// sequence starts from and Ctl, unless the run has stopped (an earlier
+// sequence's snapshot is then the one a recovery needs).
+template <typename R>
+__global__ __launch_bounds__(256) void k_seq_snap(const Ctl *ctl, const R *st0, const R *st1, R *snap, Ctl *snap_ctl,
+                                                  int64_t n)
+{
+    if (ctl->stop) return;
+    const R *cur = (ctl->done & 1) ? st1 : st0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        snap[i] = cur[i];
+    if (blockIdx.x == 0) {
+        constexpr int W = (int)(sizeof(Ctl) / sizeof(uint32_t));
+        const uint32_t *a = reinterpret_cast<const uint32_t *>(ctl);
+        uint32_t *d = reinterpret_cast<uint32_t *>(snap_ctl);
+        for (int w = threadIdx.x; w < W; w += blockDim.x) d[w] = a[w];
+    }
+}
+
+// The end of a deferred sequence of n iterations: rows [rank][n][NP] of all
+// tiles' exact totals (the all-gather of d_rows), reduced row by row in
+// iteration order and applied with fin_apply -- the trace, it / done / T and
+// the stop rule exactly as the whole grid's finalize.  A stop met before the
+// last row means the sequence's later iterations have already run: Ctl::ovr
+// = row + 1 tells the host to recover (deferred_recover).  One workgroup.
+__global__ __launch_bounds__(256) void k_finalize_seq(FinParams F, const fix128 *rows, int n)
+{
+    Ctl *ctl = F.ctl;
+    const int NP = NFIX + F.L, tid = threadIdx.x;
+    __shared__ double tot[NFIX + GQMAP_LMAX];
+    __shared__ int stopped;
+    for (int i = 0; i < n; ++i) {
+        if (tid == 0) stopped = ctl->stop;
+        __syncthreads();
+        if (stopped) return;
+        if (tid < NP) {
+            fix128 v = 0;
+            for (int r = 0; r < F.nranks; ++r) v += rows[((int64_t)r * n + i) * NP + tid];
+            tot[tid] = from_fix(v);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            fin_apply(F, tot);
+            if (ctl->stop && i < n - 1) ctl->ovr = i + 1;
+        }
+        __syncthreads();
+    }
+}
+
 // Tiled mode: this tile's block partials -> its exact totals (one row of the
 // gathered table; the other rows arrive from the other tiles).
 __global__ __launch_bounds__(256) void k_reduce_local(const fix128 *partials, int nblocks, int NP,
@@ -1823,18 +1875,36 @@ struct gqmap_ctx {
     // tiles run on `stream` (fork / join events)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_bnd = nullptr, ev_inr = nullptr, ev_xch = nullptr;
-    // speculative RCCL step (L = 1, launch_step_rccl_spec): boundary tiles on
-    // `bnd`, the exchange and the totals' all-gather on `side`, the finalize on
-    // `fin`; the totals table is double-buffered by the iteration's parity
-    // within a joined sequence (`issued`), and iteration j waits only for the
-    // finalize of iteration j - 2 (ev_fin[j & 1])
-    hipStream_t bnd = nullptr, fin = nullptr;
-    hipEvent_t ev_ag = nullptr, ev_fin[2] = {nullptr, nullptr};
-    bool fin_pending[2] = {false, false};
-    int issued = 0;
-    bool spec_now = false;      // the launches being issued belong to a speculative step
-    fix128 *gbuf = nullptr;     // this step's half of d_gathered
+    // deferred-totals RCCL step (L = 1, launch_seq_deferred): each iteration
+    // of a sequence writes this tile's exact totals to row `pos` of d_rows; the
+    // sequence ends with one all-gather of its rows into d_seqg
+    // [nranks][n][NP] and k_finalize_seq
+    fix128 *d_rows = nullptr, *d_seqg = nullptr;
+    fix128 *seq_row = nullptr;  // the row of the iteration being issued
+    bool spec_now = false;      // the launches being issued run by Ctl::it_i / done_i / T_i
 };
+
+// Execution policies that never change a result (placement, caching, launch
+// shape; tests/test_gpu_parity.py, test_gpu_persist.py hold them to the same
+// bits): chosen automatically, overridable only through the debug entry
+// gqmap_debug_policy (tests and A/B scripts; not in the public header).  The
+// library reads no environment variables.
+namespace gq {
+struct Policy {
+    int nt_state = -1;     // non-temporal state stores: -1 auto (state > 32 MiB), 0 off, 1 on
+    int band_rows = -1;    // row-by-row walk of each XCD's band: -1 auto (padded VV > 4 MiB), 0, 1
+    int cu_group = -1;     // co-resident tile grouping: -1 from the occupancy query, 0 off, n > 0 forced
+    int lpar = -1;         // super engine L > 1: -1 one block per (tile, component), 1 one block per tile
+    int lpar_xcd = 1;      // a tile's component blocks on one XCD (whole-grid fused launch)
+    int fused_finalize = 1;
+    int persist = 1;       // persistent launch of the small ctf levels
+    int persist_cap = -1;  // resident workgroups assumed by the persistent launch (-1: occupancy query)
+    int graph = 1;         // replayed hipGraphs (0: direct launches)
+    int vv_float = 1;      // float padded-frame store when exact
+    int verbose = 0;       // recovery messages on stderr
+};
+Policy g_pol;
+}  // namespace gq
 
 namespace {
 
@@ -1870,8 +1940,7 @@ int choose_split(int M, int N, int L, int forced, bool super_)
 // never changes results.  GQMAP_LPAR=1 forces one block per tile.
 int choose_lpar(const gqmap_ctx *c)
 {
-    static const char *e = std::getenv("GQMAP_LPAR");
-    if (e && *e == '1') return 1;
+    if (g_pol.lpar == 1) return 1;
     return c->super_ && c->L > 1 ? c->L : 1;
 }
 
@@ -1984,8 +2053,7 @@ FinParams fin_params(const gqmap_ctx *c);
 // reads it (round 3: NT stores on C2 +0.8%).  GQMAP_NT_STATE=0/1 forces.
 bool state_nt(const gqmap_ctx *c)
 {
-    static const char *e = std::getenv("GQMAP_NT_STATE");
-    if (e && *e) return *e == '1';
+    if (g_pol.nt_state >= 0) return g_pol.nt_state == 1;
     return (size_t)c->MNL * NPLANES * c->rsz > ((size_t)32 << 20);
 }
 
@@ -1993,16 +2061,14 @@ bool state_nt(const gqmap_ctx *c)
 // whose padded VV is larger than one XCD's 4 MiB L2.  GQMAP_BAND_ROWS=0/1 forces.
 bool band_rows(const gqmap_ctx *c)
 {
-    static const char *e = std::getenv("GQMAP_BAND_ROWS");
-    if (e && *e) return *e == '1';
+    if (g_pol.band_rows >= 0) return g_pol.band_rows == 1;
     const size_t vsz = c->fp32 ? sizeof(float) : c->vv32 ? sizeof(vvs_t) : sizeof(double);
     return vv_elems(c->Mo, c->No) * vsz > ((size_t)4 << 20);
 }
 
 bool fused_finalize(const gqmap_ctx *c)
 {
-    static const bool off = std::getenv("GQMAP_NO_FUSED_FINALIZE") != nullptr;
-    return c->nranks == 0 && !off;
+    return c->nranks == 0 && g_pol.fused_finalize;
 }
 
 template <typename R, typename VT>
@@ -2043,8 +2109,7 @@ IterParams<R, VT> iter_params(const gqmap_ctx *c)
     // k_reduce_local between the launches and the all-gather)
     P.tile_acc = c->comm != nullptr;
     P.ticket_total = c->comm ? iteration_blocks(c) : c->nblocks;
-    fix128 *gt = c->gbuf ? c->gbuf : c->d_gathered;
-    P.tile_totals = gt ? gt + (size_t)c->tile * (NFIX + c->L) : nullptr;
+    P.tile_totals = c->seq_row ? c->seq_row : c->d_gathered ? c->d_gathered + (size_t)c->tile * (NFIX + c->L) : nullptr;
     P.spec = c->spec_now ? 1 : 0;
     P.fin = fin_params(c);
     P.cu_group = 1; P.cu_slots = 32;  // set per kernel by launch_iter_q
@@ -2064,7 +2129,7 @@ FinParams fin_params(const gqmap_ctx *c)
     F.trace = c->d_trace;
     F.aepe = c->d_truth != nullptr;
     F.count = (double)(c->M - 2) * (double)(c->Ng - 2) * c->L;  // global interior
-    F.gathered = c->gbuf ? c->gbuf : c->d_gathered;
+    F.gathered = c->d_gathered;
     F.nranks = c->nranks;
     F.step0 = o.step0; F.step_decay = o.step_decay;
     F.alpha_mode = o.alpha_mode; F.alpha_start = o.alpha_start; F.alpha_lr = o.alpha_lr;
@@ -2099,14 +2164,11 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
         if (nblocks == 0) return;
     }
     static const int2 shape = kernel_shape(k_iter<R, VT, ENG, Q>);
-    if (!getenv("GQMAP_NO_CU_GROUP")) {
-        P.cu_group = shape.x;
+    if (g_pol.cu_group != 0) {
+        P.cu_group = g_pol.cu_group > 0 ? g_pol.cu_group : shape.x;
         P.cu_slots = std::max(1, shape.y / 8);
-        if (const char *g = getenv("GQMAP_CU_GROUP")) P.cu_group = atoi(g);
-        if (getenv("GQMAP_CU_GROUP_PRINT")) fprintf(stderr, "k_iter Q=%d cu_group %d cu_slots %d\n", Q, P.cu_group, P.cu_slots);
     }
-    static const bool lpar_xcd = !getenv("GQMAP_NO_LPAR_XCD");
-    if (c->lpar > 1 && P.fused && !sg && lpar_xcd) {
+    if (c->lpar > 1 && P.fused && !sg && g_pol.lpar_xcd) {
         P.lpar_xcd = 1;
         nblocks = 8 * c->lpar * ((c->tiles_m * c->tiles_n + 7) / 8);
     }
@@ -2216,11 +2278,10 @@ int persist_capacity()
         // take one wave slot per SIMD each, as the API counts them
         if (Q == 64) per_cu = std::min(per_cu, 1);
         cap = std::max(0, per_cu) * std::max(0, cus);
-        // GQMAP_PERSIST_CAP=n: resident workgroups assumed (tests force the
-        // per-iteration path with a capacity too small for the grid)
-        if (const char *e = std::getenv("GQMAP_PERSIST_CAP")) cap = atoi(e);
     }
-    return cap;
+    // policy persist_cap: resident workgroups assumed (tests force the
+    // per-iteration path with a capacity too small for the grid)
+    return g_pol.persist_cap >= 0 ? g_pol.persist_cap : cap;
 }
 
 // The snapshot buffers of the persistent path (allocated outside a capture;
@@ -2263,8 +2324,7 @@ bool launch_persist_q(gqmap_ctx *c, int n, bool dry)
     P.fin.nblocks = 2 * G;  // partial row stride: iteration j writes rows (j & 1) * G + b
     const int threads = Q == 64 ? WN_THREADS : BLOCK;
     static const int2 shape = kernel_shape(k_iter_persist<R, VT, 2, Q>);
-    static const bool no_group = std::getenv("GQMAP_NO_CU_GROUP") != nullptr;
-    P.cu_group = Q == 64 || no_group ? 1 : shape.x;
+    P.cu_group = Q == 64 || g_pol.cu_group == 0 ? 1 : g_pol.cu_group > 0 ? g_pol.cu_group : shape.x;
     P.cu_slots = std::max(1, shape.y / 8);
     k_iter_persist<R, VT, 2, Q><<<G + 1, threads, 0, c->stream>>>(P, n);
     return true;
@@ -2290,8 +2350,7 @@ bool launch_persist_t(gqmap_ctx *c, int n, bool dry)
 // dry: only the check
 bool launch_persist(gqmap_ctx *c, int n, bool dry = false)
 {
-    static const bool off = std::getenv("GQMAP_NO_PERSIST") != nullptr;
-    if (off || c->persist_off || c->opt.engine != GQMAP_ENGINE_CTF || c->L != 1 || c->n_tiles != 1 || c->comm || c->nranks != 0 ||
+    if (!g_pol.persist || c->persist_off || c->opt.engine != GQMAP_ENGINE_CTF || c->L != 1 || c->n_tiles != 1 || c->comm || c->nranks != 0 ||
         !fused_finalize(c) || n < 1)
         return false;
     if (c->fp32) return launch_persist_t<float, float>(c, n, dry);
@@ -2473,29 +2532,32 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     return GQMAP_OK;
 }
 
-// Speculative RCCL step for L = 1 (rccl_spec below).  Nothing of iteration j + 1 depends on iteration j's totals
-// but the stop rule, so the all-gather of the totals and the finalize leave
-// the critical path: per iteration
-//   main  [wait finalize(j-2)] fork | interior k_iter | wait exchange | unpack + advance (k_unpack_advance)
-//   bnd   boundary k_iter, pack
-//   side  send/recv (after pack) | all-gather of the totals (after both k_iter launches)
-//   fin   k_finalize (after the all-gather): trace, T / it / done, stop rule
-// Iteration j + 1 may run before finalize(j) has judged iteration j: if j met
-// the rule, j + 1 wrote only the buffer that held state j - 1 (Ctl::done still
-// points at state j) and finalize(j + 1) returns on the stop flag; iteration
-// j + 2 waits for finalize(j) and turns into no-ops.  RCCL calls stay on one
-// stream in one order on every rank.  Totals of iteration j live in half
-// (j & 1) of d_gathered: half j & 1 is rewritten by iteration j + 2, which
-// starts after finalize(j).
-// Opt-in (GQMAP_SPEC=1): behind a one-rank communicator it measured no gain
-// (profiles/r03_strip_spec.txt), and its cross-rank behaviour (ranks judging
-// the stop rule at different points of iteration j + 1) has not run with a
-// second GPU yet -- the default multi-rank step is launch_step_rccl.
-bool rccl_spec(const gqmap_ctx *c)
+// Deferred-totals RCCL step (L = 1).  Nothing of iteration j + 1 depends on
+// iteration j's totals but the stop rule (alpha is constant, the step size
+// and the temperature decay follow the iteration number), so the totals'
+// all-gather and the finalize leave the iteration: per iteration only
+//   main  fork | interior k_iter               | wait exchange | unpack + advance
+//   side        boundary k_iter, pack, send/recv | (ev_xch)
+// with this tile's exact totals of iteration pos written to row pos of
+// d_rows by the last workgroup of the two k_iter launches, and the kernels
+// running by Ctl::it_i / done_i / T_i (k_unpack_advance takes fin_apply's
+// steps for them).  A sequence of n <= GRAPH_CHUNK iterations
+//   k_seq_snap (state + Ctl, unless stopped) | n iterations |
+//   one all-gather of the n rows | k_finalize_seq (fin_apply per row: the
+//   trace, it / done / T, the stop rule)
+// is one captured graph.  If row i < n - 1 met the stop rule, iterations
+// i + 1 .. n - 1 have already run: k_finalize_seq records Ctl::ovr = i + 1,
+// later sequences turn into no-ops (Ctl::stop), and the host restores the
+// snapshot and re-runs the i + 1 iterations with the exact per-iteration
+// step (deferred_recover) -- the same state, trace and stop iteration as the
+// whole grid.  Every stream capture below records an event and has it waited
+// on before the event is recorded again (the pattern of launch_step_rccl;
+// DESIGN.md 5 on HIP's capture).
+// (the snapshot buffers are allocated outside any capture -- gqmap_tile_attach_rccl,
+// capture_steps -- and follow the grid size; without them the exact step runs)
+bool deferred(const gqmap_ctx *c)
 {
-    if (!c->comm || c->L != 1) return false;
-    const char *e = std::getenv("GQMAP_SPEC");
-    return e && *e == '1';
+    return c->comm && c->L == 1 && c->d_rows && c->d_snap && c->snap_bytes == (size_t)c->MNL * NPLANES * c->rsz;
 }
 
 template <typename R>
@@ -2511,79 +2573,110 @@ void unpack_advance_t(gqmap_ctx *c)
                                                   c->opt.t_decay_every, c->opt.drate, c->opt.t_min);
 }
 
-gqmap_status launch_step_rccl_spec(gqmap_ctx *c)
+// Iteration `pos` of a deferred sequence; e0 / e1 (optional) bracket the two
+// k_iter launches.
+gqmap_status launch_step_deferred(gqmap_ctx *c, int pos, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
-    const int NP = NFIX + c->L, r = c->comm->rank;
+    const int r = c->comm->rank;
     const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
     const size_t nl = (size_t)HALO_TO_LEFT_N * c->L * c->M, nr = (size_t)HALO_TO_RIGHT_N * c->L * c->M;
     const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
     const Rccl *R = rccl();
     TileSegs bnd, inr;
     tile_segments(c, bnd, inr);
-    const int par = c->issued & 1;
-    c->issued++;
-    c->gbuf = c->d_gathered + (size_t)par * c->n_tiles * NP;
     c->spec_now = true;
+    c->seq_row = c->d_rows + (size_t)pos * (NFIX + c->L);
     hipStream_t main_stream = c->stream;
-    // the stop verdict on iteration j - 2 before iteration j starts
-    if (c->fin_pending[par]) GQ_HIP(hipStreamWaitEvent(main_stream, c->ev_fin[par], 0));
+    if (e0) GQ_HIP(hipEventRecord(e0, main_stream));
     GQ_HIP(hipEventRecord(c->ev_fork, main_stream));
-    GQ_HIP(hipStreamWaitEvent(c->bnd, c->ev_fork, 0));
-    c->stream = c->bnd;
+    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    c->stream = c->side;
     launch_iter(c, &bnd);
-    halo_pack(c, c->bnd);
     c->stream = main_stream;
-    GQ_HIP(hipEventRecord(c->ev_bnd, c->bnd));
-    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_bnd, 0));
-    GQ_NCCL(R->GroupStart());
-    if (left) {
-        GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->side));
-        GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->side));
+    GQ_HIP(hipEventRecord(c->ev_bnd, c->side));
+    halo_pack(c, c->side);
+    if (left || right) {
+        GQ_NCCL(R->GroupStart());
+        if (left) {
+            GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->side));
+            GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->side));
+        }
+        if (right) {
+            GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->side));
+            GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->side));
+        }
+        GQ_NCCL(R->GroupEnd());
     }
-    if (right) {
-        GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->side));
-        GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->side));
-    }
-    GQ_NCCL(R->GroupEnd());
     GQ_HIP(hipEventRecord(c->ev_xch, c->side));
     launch_iter(c, &inr);
-    GQ_HIP(hipEventRecord(c->ev_inr, main_stream));
-    // the totals (written by the last workgroup of the two launches)
-    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_inr, 0));
-    GQ_NCCL(R->AllGather(c->gbuf + (size_t)r * NP, c->gbuf, (size_t)NP * sizeof(fix128), ncclUint8, c->comm->comm,
-                         c->side));
-    GQ_HIP(hipEventRecord(c->ev_ag, c->side));
-    GQ_HIP(hipStreamWaitEvent(c->fin, c->ev_ag, 0));
-    k_finalize<<<1, 256, 0, c->fin>>>(fin_params(c));
-    GQ_HIP(hipEventRecord(c->ev_fin[par], c->fin));
-    c->fin_pending[par] = true;
+    if (e1) {
+        GQ_HIP(hipStreamWaitEvent(main_stream, c->ev_bnd, 0));
+        GQ_HIP(hipEventRecord(e1, main_stream));
+    }
     GQ_HIP(hipStreamWaitEvent(main_stream, c->ev_xch, 0));
     if (c->fp32) unpack_advance_t<float>(c);
     else unpack_advance_t<double>(c);
     c->spec_now = false;
-    c->gbuf = nullptr;
+    c->seq_row = nullptr;
     return GQMAP_OK;
 }
 
-// The end of a speculative sequence: every finalize joined into the context
-// stream (also what a stream capture needs to close), parity restarts.
-gqmap_status join_spec(gqmap_ctx *c)
+// A deferred sequence of n (1..GRAPH_CHUNK) iterations; ev (optional): 2 n
+// events, a pair around each iteration's k_iter launches.
+gqmap_status launch_seq_deferred(gqmap_ctx *c, int n, hipEvent_t *ev = nullptr)
 {
-    for (int p = 0; p < 2; ++p)
-        if (c->fin_pending[p]) {
-            GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_fin[p], 0));
-            c->fin_pending[p] = false;
-        }
-    c->issued = 0;
-    c->spec_now = false;
-    c->gbuf = nullptr;
+    const int NP = NFIX + c->L;
+    {
+        const int64_t nv = (int64_t)c->MNL * NPLANES;
+        const int grid = (int)std::min<int64_t>((nv + 255) / 256, 512);
+        if (c->fp32)
+            k_seq_snap<float><<<grid, 256, 0, c->stream>>>(c->d_ctl, (const float *)c->d_st[0], (const float *)c->d_st[1],
+                                                           (float *)c->d_snap, c->d_snap_ctl, nv);
+        else
+            k_seq_snap<double><<<grid, 256, 0, c->stream>>>(c->d_ctl, (const double *)c->d_st[0],
+                                                            (const double *)c->d_st[1], (double *)c->d_snap,
+                                                            c->d_snap_ctl, nv);
+    }
+    for (int i = 0; i < n; ++i) {
+        gqmap_status st = launch_step_deferred(c, i, ev ? ev[2 * i] : nullptr, ev ? ev[2 * i + 1] : nullptr);
+        if (st != GQMAP_OK) return st;
+    }
+    const Rccl *R = rccl();
+    GQ_NCCL(R->AllGather(c->d_rows, c->d_seqg, (size_t)n * NP * sizeof(fix128), ncclUint8, c->comm->comm,
+                         c->stream));
+    k_finalize_seq<<<1, 256, 0, c->stream>>>(fin_params(c), c->d_seqg, n);
+    return GQMAP_OK;
+}
+
+// After a run: a deferred sequence overshot its stop iteration (Ctl::ovr):
+// restore the sequence's snapshot (state + Ctl at its start) and re-run its
+// first ovr iterations with the exact per-iteration step, which stops at the
+// same iteration as the whole grid.  Every rank sees the same all-gathered
+// totals, so every rank recovers together (the re-run's collectives match).
+gqmap_status deferred_recover(gqmap_ctx *c, const Ctl &h, bool *recovered)
+{
+    *recovered = false;
+    if (!deferred(c) || h.ovr == 0) return GQMAP_OK;
+    c->ctl_known = false;
+    Ctl snap;
+    GQ_HIP(hipMemcpyAsync(&snap, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    GQ_HIP(hipMemcpyAsync(c->d_st[snap.done & 1], c->d_snap, (size_t)c->MNL * NPLANES * c->rsz, hipMemcpyDeviceToDevice,
+                          c->stream));
+    GQ_HIP(hipMemcpyAsync(c->d_ctl, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToDevice, c->stream));
+    for (int i = 0; i < h.ovr; ++i) {
+        gqmap_status st = launch_step_rccl(c);
+        if (st != GQMAP_OK) return st;
+    }
+    GQ_HIP(hipStreamSynchronize(c->stream));
+    *recovered = true;
     return GQMAP_OK;
 }
 
 gqmap_status launch_step(gqmap_ctx *c)
 {
     c->ctl_known = false;
-    if (c->comm) return rccl_spec(c) ? launch_step_rccl_spec(c) : launch_step_rccl(c);
+    if (c->comm) return launch_step_rccl(c);
     launch_iter(c);
     return launch_tail(c);
 }
@@ -2594,8 +2687,11 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
     c->ctl_known = false;
     if (launch_persist(c, n)) return GQMAP_OK;
     gqmap_status st = GQMAP_OK;
+    if (deferred(c)) {
+        for (int i = 0; i < n && st == GQMAP_OK; i += GRAPH_CHUNK) st = launch_seq_deferred(c, std::min(GRAPH_CHUNK, n - i));
+        return st;
+    }
     for (int i = 0; i < n && st == GQMAP_OK; ++i) st = launch_step(c);
-    if (st == GQMAP_OK && rccl_spec(c)) st = join_spec(c);
     return st;
 }
 
@@ -2627,7 +2723,7 @@ gqmap_status persist_recover(gqmap_ctx *c, bool *recovered)
     GQ_HIP(hipMemcpyAsync(c->d_ctl, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToDevice, c->stream));
     GQ_HIP(hipMemsetAsync(c->d_bar, 0, sizeof(unsigned) * BAR_WORDS, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
-    if (std::getenv("GQMAP_PERSIST_VERBOSE"))
+    if (g_pol.verbose)
         fprintf(stderr, "gqmap: persistent launch failed (%d workgroups); restored iteration %d, "
                         "continuing with one launch per iteration\n", c->nblocks + 1, h.it);
     c->persist_off = true;
@@ -2652,6 +2748,9 @@ gqmap_status upload_ctl(gqmap_ctx *c, int it, double T, const double *w, const d
     }
     c->ctl_known = false;
     GQ_HIP(hipMemcpyAsync(c->d_ctl, &h, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
+    // a new state: a persistent launch's failure word (and the snapshot it
+    // guards) belongs to the old one (persist_recover would restore it)
+    GQ_HIP(hipMemsetAsync(c->d_bar + BAR_FAIL, 0, sizeof(unsigned), c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     c->ctl_it = it;
     c->ctl_known = true;
@@ -2703,6 +2802,7 @@ gqmap_status capture_steps(gqmap_ctx *c, int n, hipGraphExec_t *out)
 {
     if (*out) return GQMAP_OK;
     (void)launch_persist(c, n, true);  // occupancy query, snapshot buffers: outside the capture
+    if (c->comm && c->L == 1) (void)ensure_snap(c);  // the deferred RCCL sequence's snapshot
     hipGraph_t g;
     GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     gqmap_status st = launch_steps(c, n);
@@ -2832,7 +2932,7 @@ gqmap_status ctx_set_images_device(gqmap_ctx *c, const double *dI1, const double
     GQ_HIP(pad_vv_device(dI2, Mo, No, d_scratch, c->stream));
     const size_t nvv = (size_t)(Mo + 2) * (No + 2);
     bool vv32 = c->fp32;
-    if (!vv32 && !std::getenv("GQMAP_VV64"))
+    if (!vv32 && g_pol.vv_float)
         GQ_HIP(f32_exact_device(d_scratch, nvv, d_flag, &vv32, c->stream));
     gqmap_status s = prepare_images(c, Mo, No, vv32);
     if (s != GQMAP_OK) return s;
@@ -3061,7 +3161,7 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
     // from rgb2gray are integers; their cubic padding stays in [-510, 765]):
     // same values, half the gather bytes.
     bool vv32 = c->fp32;
-    if (!vv32 && !std::getenv("GQMAP_VV64")) {
+    if (!vv32 && g_pol.vv_float) {
         vv32 = true;
         for (double v : VV)
             if ((double)(vvs_t)v != v) { vv32 = false; break; }
@@ -3256,6 +3356,7 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
              c->n_tiles);
     GQ_CHECK(n_iter >= 0, GQMAP_ERR_INVALID_ARG, "n_iter < 0");
     DeviceGuard dg(c->device);
+    if (c->comm && c->L == 1) (void)ensure_snap(c);  // deferred RCCL sequences (outside any capture)
     Ctl h0;
     gqmap_status s = GQMAP_OK;
     if (c->ctl_known) h0.it = c->ctl_it;
@@ -3266,8 +3367,7 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         const int chunk = std::min(n_iter - total, TRACE_CAP);
         int left = chunk;
         c->ctl_known = false;
-        static const bool no_graph = std::getenv("GQMAP_NO_GRAPH") != nullptr;
-        if (!no_graph) {
+        if (g_pol.graph) {
             // GRAPH_CHUNK-iteration graphs, then the remainder as graphs of
             // 2^k iterations (a short run replays graphs too)
             if (left >= GRAPH_CHUNK && (s = ensure_graph(c)) != GQMAP_OK) return s;
@@ -3294,9 +3394,19 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         GQ_HIP(hipStreamSynchronize(c->stream));
         Ctl h = *c->h_ctl;
         bool recovered = false;
-        if (c->d_snap && *c->h_fail != 0) {
+        if (c->d_snap && !c->comm && *c->h_fail != 0) {
             if ((s = persist_recover(c, &recovered)) != GQMAP_OK) return s;
             if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+        }
+        if (h.ovr) {  // a deferred RCCL sequence ran past its stop iteration
+            bool again = false;
+            if ((s = deferred_recover(c, h, &again)) != GQMAP_OK) return s;
+            if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+            // (the finalize had already recorded the trace up to the stop; the
+            // exact re-run rewrote the same slots -- read them again anyway)
+            if ((trace || aepe) && (s = queue_trace(c, it_first, std::min(chunk, std::max(0, h.it - it_first)))) != GQMAP_OK)
+                return s;
+            GQ_HIP(hipStreamSynchronize(c->stream));
         }
         const int ran = h.it - it_first;
         copy_trace(c, it_first, std::min(ran, chunk), trace ? trace + 3 * total : nullptr, aepe ? aepe + total : nullptr);
@@ -3320,21 +3430,27 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
              c->n_tiles);
     GQ_CHECK(n_iter >= 1, GQMAP_ERR_INVALID_ARG, "n_iter < 1");
     DeviceGuard dg(c->device);
+    if (c->comm && c->L == 1) (void)ensure_snap(c);
     Ctl h0;
     gqmap_status s = read_ctl(c, &h0);
     if (s != GQMAP_OK) return s;
     std::vector<hipEvent_t> ev((size_t)2 * n_iter + 2);
     for (auto &e : ev) GQ_HIP(hipEventCreate(&e));
     GQ_HIP(hipEventRecord(ev[0], c->stream));
-    for (int i = 0; i < n_iter; ++i) {
-        if (c->comm) {  // both k_iter launches (boundary, interior) of the iteration
-            if ((s = launch_step_rccl(c, ev[2 + 2 * i], ev[3 + 2 * i])) != GQMAP_OK) return s;
-            continue;
+    if (deferred(c)) {  // the production sequences, both k_iter launches of each iteration bracketed
+        for (int i = 0; i < n_iter; i += GRAPH_CHUNK)
+            if ((s = launch_seq_deferred(c, std::min(GRAPH_CHUNK, n_iter - i), &ev[2 + 2 * i])) != GQMAP_OK) return s;
+    } else {
+        for (int i = 0; i < n_iter; ++i) {
+            if (c->comm) {  // both k_iter launches (boundary, interior) of the iteration
+                if ((s = launch_step_rccl(c, ev[2 + 2 * i], ev[3 + 2 * i])) != GQMAP_OK) return s;
+                continue;
+            }
+            GQ_HIP(hipEventRecord(ev[2 + 2 * i], c->stream));
+            launch_iter(c);
+            GQ_HIP(hipEventRecord(ev[3 + 2 * i], c->stream));
+            if ((s = launch_tail(c)) != GQMAP_OK) return s;
         }
-        GQ_HIP(hipEventRecord(ev[2 + 2 * i], c->stream));
-        launch_iter(c);
-        GQ_HIP(hipEventRecord(ev[3 + 2 * i], c->stream));
-        if ((s = launch_tail(c)) != GQMAP_OK) return s;
     }
     GQ_HIP(hipEventRecord(ev[1], c->stream));
     GQ_HIP(hipEventSynchronize(ev[1]));
@@ -3350,6 +3466,11 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     for (auto &e : ev) (void)hipEventDestroy(e);
     Ctl h;
     if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+    if (h.ovr) {
+        bool again = false;
+        if ((s = deferred_recover(c, h, &again)) != GQMAP_OK) return s;
+        if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+    }
     if (n_done) *n_done = h.it - h0.it;
     if (total_ms) *total_ms = t;
     if (iter_kernel_ms) *iter_kernel_ms = sum;
@@ -3415,6 +3536,30 @@ gqmap_status gqmap_debug_persist_fault(gqmap_ctx *c, int j)
 // Not in the public header (tests): 1 when the context has fallen back from
 // the persistent launch to one launch per iteration.
 int gqmap_debug_persist_off(const gqmap_ctx *c) { return c && c->persist_off ? 1 : 0; }
+
+// Not in the public header (tests, A/B scripts): set one execution policy of
+// gq::Policy by name, process-wide; contexts created (or graphs captured)
+// afterwards use it.  value -1 restores the automatic choice where there is
+// one.  Returns 0, or -1 for an unknown name.
+int gqmap_debug_policy(const char *name, int value)
+{
+    if (!name) return -1;
+    struct Field { const char *n; int *p; int dflt; };
+    const Field fields[] = {
+        {"nt_state", &g_pol.nt_state, -1},   {"band_rows", &g_pol.band_rows, -1},
+        {"cu_group", &g_pol.cu_group, -1},   {"lpar", &g_pol.lpar, -1},
+        {"lpar_xcd", &g_pol.lpar_xcd, 1},    {"fused_finalize", &g_pol.fused_finalize, 1},
+        {"persist", &g_pol.persist, 1},      {"persist_cap", &g_pol.persist_cap, -1},
+        {"graph", &g_pol.graph, 1},          {"vv_float", &g_pol.vv_float, 1},
+        {"verbose", &g_pol.verbose, 0},
+    };
+    for (const Field &f : fields)
+        if (std::strcmp(f.n, name) == 0) {
+            *f.p = value == -1 ? f.dflt : value;
+            return 0;
+        }
+    return -1;
+}
 
 gqmap_status gqmap_get_info(gqmap_ctx *c, gqmap_info *info)
 {
@@ -3631,10 +3776,14 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
     gqmap_status s = attach_common(c);
     if (s != GQMAP_OK) return s;
     GQ_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    GQ_HIP(hipStreamCreateWithFlags(&c->bnd, hipStreamNonBlocking));
-    GQ_HIP(hipStreamCreateWithFlags(&c->fin, hipStreamNonBlocking));
-    for (hipEvent_t *e : {&c->ev_fork, &c->ev_bnd, &c->ev_inr, &c->ev_xch, &c->ev_ag, &c->ev_fin[0], &c->ev_fin[1]})
+    for (hipEvent_t *e : {&c->ev_fork, &c->ev_bnd, &c->ev_inr, &c->ev_xch})
         GQ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    if (c->L == 1) {  // deferred-totals sequences (launch_seq_deferred)
+        const size_t NP = NFIX + c->L;
+        GQ_HIP(hipMalloc((void **)&c->d_rows, sizeof(fix128) * NP * GRAPH_CHUNK));
+        GQ_HIP(hipMalloc((void **)&c->d_seqg, sizeof(fix128) * NP * GRAPH_CHUNK * c->n_tiles));
+        (void)ensure_snap(c);
+    }
     return GQMAP_OK;
 }
 
@@ -3812,12 +3961,12 @@ void gqmap_destroy(gqmap_ctx *c)
         (void)rccl()->CommDestroy(c->comm->comm);
         delete c->comm;
     }
-    for (hipStream_t st : {c->side, c->bnd, c->fin})
-        if (st) (void)hipStreamSynchronize(st);
-    for (hipEvent_t e : {c->ev_fork, c->ev_bnd, c->ev_inr, c->ev_xch, c->ev_ag, c->ev_fin[0], c->ev_fin[1]})
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    for (hipEvent_t e : {c->ev_fork, c->ev_bnd, c->ev_inr, c->ev_xch})
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t st : {c->side, c->bnd, c->fin})
-        if (st) (void)hipStreamDestroy(st);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    for (void *p : {(void *)c->d_rows, (void *)c->d_seqg})
+        if (p) (void)hipFree(p);
     if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);

@@ -247,6 +247,23 @@ def test_full_rubberwhale_500_iterations_bit_exact():
     assert a_gpu == a_cpu
 
 
+class _policy:
+    """Execution policies (gqmap_debug_policy) for the duration of a block."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        from gqmap_opticalflow_amd import _lib
+        for k, v in self.kw.items():
+            _lib.debug_policy(k, v)
+
+    def __exit__(self, *a):
+        from gqmap_opticalflow_amd import _lib
+        for k in self.kw:
+            _lib.debug_policy(k, -1)
+
+
 def _run_engine(o, I1, I2, engine, precision, st, its):
     from gqmap_opticalflow_amd import Engine
     with Engine(o, I1, I2, engine, precision) as eng:
@@ -280,13 +297,13 @@ def test_single_gaussian_every_split_bit_exact_vs_emulator(engine, K, M, N, spli
     _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
 
 
-def test_graph_replay_equals_per_iteration_launches(monkeypatch):
+def test_graph_replay_equals_per_iteration_launches():
     # full C2 frame, 120 iterations: 2 captured 50-iteration graphs + 20
-    # single launches against 120 single launches (GQMAP_NO_GRAPH)
+    # single launches against 120 single launches (policy graph = 0)
     I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 388, 584)
     a = _run_engine(o, I1, I2, "mixture", "fp64", st, 120)
-    monkeypatch.setenv("GQMAP_NO_GRAPH", "1")
-    b = _run_engine(o, I1, I2, "mixture", "fp64", st, 120)
+    with _policy(graph=0):
+        b = _run_engine(o, I1, I2, "mixture", "fp64", st, 120)
     assert a[0] == b[0] == 120
     np.testing.assert_array_equal(a[1], b[1])
     for k in G.STATE_KEYS:
@@ -473,57 +490,58 @@ def test_super_bit_exact_on_preprocessed_frames(precision):
     _assert_bit_exact(g, tr, done, e_done, e_tr, ost)
 
 
-def test_nontemporal_state_stores_same_bits():
-    # state_nt (non-temporal state stores, and own-state loads where built
-    # in) is a cache policy: forced on, a C2 crop gives the same trace and
-    # state as forced off (separate processes: the policy is read once)
-    import os
-    import subprocess
-    import sys
-    import tempfile
-    code = r'''
-import sys, numpy as np
-sys.path.insert(0, ".")
-from tests.test_gpu_parity import _reference_init_case, _run_engine
-I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 128, 160, 100, 150, L=1, K=9)
-_, tr, g, _ = _run_engine(o, I1, I2, "mixture", "fp64", st, 60)
-np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigu.ravel(), g.pn.ravel(), g.rou.ravel()]))
-'''
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with tempfile.TemporaryDirectory() as d:
-        outs = []
-        for v in ("0", "1"):
-            env = dict(os.environ, GQMAP_NT_STATE=v)
-            f = os.path.join(d, f"nt{v}.npy")
-            subprocess.run([sys.executable, "-c", code, f], cwd=root, env=env, check=True, timeout=300)
-            outs.append(np.load(f))
-    np.testing.assert_array_equal(outs[0], outs[1])
+def _placement_runs(o, I1, I2, engine, precision, st, its, split, policies):
+    """The same run under each policy setting (gqmap_debug_policy): a list of
+    (trace, state); each run asserts the lanes per node it was meant to use."""
+    outs = []
+    for pol in policies:
+        with _policy(**pol):
+            done, tr, g, info = _run_engine(dict(o, split=split), I1, I2, engine, precision, st, its)
+        assert info.split == split and done == its
+        outs.append((tr, g))
+    return outs
+
+
+def _same_runs(outs):
+    for tr, g in outs[1:]:
+        np.testing.assert_array_equal(tr, outs[0][0])
+        for k in G.STATE_KEYS:
+            np.testing.assert_array_equal(getattr(g, k), getattr(outs[0][1], k), err_msg=k)
+
+
+@pytest.mark.parametrize("engine", ["mixture", "ctf"])
+def test_nontemporal_state_stores_same_bits(engine):
+    # state_nt (non-temporal state stores) is a cache policy: forced on, a
+    # crop at split 1 -- the only split whose kernel has the NT variant
+    # (k_iter<..,Q=1,NT=true>; the default for frames whose state exceeds
+    # 32 MiB, C5 and the large ctf levels) -- gives the trace and state of
+    # forced off, and both equal the CPU model
+    I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 128, 160, 100, 150, L=1, K=9 if engine == "mixture"
+                                               else 11, engine=engine)
+    outs = _placement_runs(o, I1, I2, engine, "fp64", st, 60, 1, [dict(nt_state=0), dict(nt_state=1)])
+    _same_runs(outs)
+    e_done, e_tr, _, ost = _emulate(o, I1, I2, st, 60, "fp64", 1)
+    _assert_bit_exact(outs[1][1], outs[1][0], 60, e_done, e_tr, ost)
 
 
 @pytest.mark.parametrize("precision", ["fp64", "fp32"])
-def test_band_row_tile_order_same_bits(precision):
-    # GQMAP_BAND_ROWS (each XCD walks its band of tile columns row by row,
+@pytest.mark.parametrize("split", [1, 4])
+def test_band_row_tile_order_same_bits(precision, split):
+    # band_rows (each XCD walks its band of tile columns row by row,
     # gqmap_engine.hip band_row_tile) is a placement: forced on, a 100 x 150
-    # frame (7 tile rows, 10 tile columns: the bands start and end inside a
-    # tile column) gives the same trace and state as forced off
-    import os
-    import subprocess
-    import sys
-    import tempfile
-    code = r'''
-import sys, numpy as np
-sys.path.insert(0, ".")
-from tests.test_gpu_parity import _reference_init_case, _run_engine
-I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 100, 150, 100, 150, L=2, K=9)
-_, tr, g, _ = _run_engine(o, I1, I2, "mixture", sys.argv[2], st, 60)
-np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigu.ravel(), g.pn.ravel(), g.rou.ravel()]))
-'''
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with tempfile.TemporaryDirectory() as d:
-        outs = []
-        for v in ("0", "1"):
-            env = dict(os.environ, GQMAP_BAND_ROWS=v)
-            f = os.path.join(d, f"band{v}.npy")
-            subprocess.run([sys.executable, "-c", code, f, precision], cwd=root, env=env, check=True, timeout=300)
-            outs.append(np.load(f))
-    np.testing.assert_array_equal(outs[0], outs[1])
+    # frame -- at split 1 16 x 16 tiles, 7 tile rows x 10 tile columns; at
+    # split 4 8 x 8 tiles, 13 x 19: the bands start and end inside a tile
+    # column -- gives the trace and state of forced off
+    I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 100, 150, 100, 150, L=2, K=9)
+    _same_runs(_placement_runs(o, I1, I2, "mixture", precision, st, 60, split,
+                               [dict(band_rows=0), dict(band_rows=1)]))
+
+
+def test_c5_default_policies_together_same_bits():
+    # the C5 default combination -- non-temporal stores and the band-row walk
+    # together, on the ctf engine (ENG = 2) and the mixture engine at split 1
+    # -- against both off
+    for engine, K in (("ctf", 11), ("mixture", 9)):
+        I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 100, 150, 100, 150, L=1, K=K, engine=engine)
+        _same_runs(_placement_runs(o, I1, I2, engine, "fp64", st, 40, 1,
+                                   [dict(nt_state=0, band_rows=0), dict(nt_state=1, band_rows=1)]))

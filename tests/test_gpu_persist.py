@@ -117,30 +117,14 @@ def test_persistent_failure_recovers_bit_exact(split, barrier):
 
 
 def test_persistent_capacity_override_runs_per_iteration():
-    # GQMAP_PERSIST_CAP: a capacity too small for the grid keeps the level on
+    # policy persist_cap: a capacity too small for the grid keeps the level on
     # one launch per iteration (the path a device without room takes) -- the
     # same bits as the persistent launch
-    import subprocess
-    import sys
-    code = r'''
-import sys, numpy as np
-sys.path.insert(0, ".")
-from tests.test_gpu_parity import _reference_init_case, _run_engine
-I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 30, 40, 150, 200, L=1, K=11, engine="ctf", split=64)
-_, tr, g, _ = _run_engine(o, I1, I2, "ctf", "fp64", st, 70)
-np.save(sys.argv[1], np.concatenate([tr.ravel(), g.muu.ravel(), g.sigv.ravel(), g.rou.ravel()]))
-'''
-    import os
-    import tempfile
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with tempfile.TemporaryDirectory() as d:
-        outs = []
-        for cap in (None, "1"):
-            env = dict(os.environ)
-            env.pop("GQMAP_PERSIST_CAP", None)
-            if cap:
-                env["GQMAP_PERSIST_CAP"] = cap
-            f = os.path.join(d, f"r{cap}.npy")
-            subprocess.run([sys.executable, "-c", code, f], cwd=root, env=env, check=True, timeout=300)
-            outs.append(np.load(f))
+    from tests.test_gpu_parity import _policy, _reference_init_case, _run_engine
+    I1, I2, _, _, o, st = _reference_init_case("rubberwhale", 30, 40, 150, 200, L=1, K=11, engine="ctf", split=64)
+    outs = []
+    for cap in (-1, 1):
+        with _policy(persist_cap=cap):
+            _, tr, g, _ = _run_engine(o, I1, I2, "ctf", "fp64", st, 70)
+        outs.append(np.concatenate([tr.ravel(), g.muu.ravel(), g.sigv.ravel(), g.rou.ravel()]))
     np.testing.assert_array_equal(outs[0], outs[1])

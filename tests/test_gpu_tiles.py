@@ -244,15 +244,14 @@ def test_c2_pair_strips_at_per_strip_split_bit_exact(n_tiles):
             t.close()
 
 
-def test_single_rank_rccl_speculative_step_l1(monkeypatch):
-    """L = 1 RCCL tiles take the speculative step (launch_step_rccl_spec: the
-    totals' all-gather and the finalize off the critical path, the stop rule
-    judged one iteration behind; forced on for one rank, the default with
-    more): bit-identical to the whole grid over replayed graphs + leftover
-    launches with the temperature decay on, and a run_timed (the
-    non-speculative step) in between keeps the counters."""
+def test_single_rank_rccl_deferred_step_l1():
+    """L = 1 RCCL tiles run deferred-totals sequences (launch_seq_deferred:
+    per iteration only the k_iter launches, the exchange and the unpack; the
+    totals of a whole sequence all-gathered once and finalized row by row at
+    its end): bit-identical to the whole grid over replayed graphs + leftover
+    sequences with the temperature decay on, and a run_timed (the same
+    sequences, instrumented) in between keeps the counters."""
     from gqmap_opticalflow_amd import Engine, comm_unique_id
-    monkeypatch.setenv("GQMAP_SPEC", "1")
     I1, I2, o = _problem("mixture", 1)
     o = dict(o, temperature=0.3, t_decay_every=7)
     init, ref, tr = _whole(I1, I2, o, "mixture", "fp64", 133, seed=1)
@@ -275,12 +274,12 @@ def test_single_rank_rccl_speculative_step_l1(monkeypatch):
 
 
 @pytest.mark.parametrize("k", [0, 23, 49, 57])
-def test_single_rank_rccl_speculative_stop(k, monkeypatch):
+def test_single_rank_rccl_deferred_stop(k):
     # the stop rule met at row k (inside a graph chunk, at its last iteration,
-    # in the leftover launches): the speculative iteration after it leaves no
-    # trace; the state is the whole grid's after k + 1 iterations
+    # in the leftover sequence): the sequence's iterations after it are undone
+    # (snapshot + exact re-run, deferred_recover); the state and trace are the
+    # whole grid's after k + 1 iterations
     from gqmap_opticalflow_amd import Engine, comm_unique_id
-    monkeypatch.setenv("GQMAP_SPEC", "1")
     I1, I2, o = _problem("mixture", 1)
     init, _, tr = _whole(I1, I2, o, "mixture", "fp64", 70, seed=1)
     ptd = tr[:, 1]
@@ -299,5 +298,29 @@ def test_single_rank_rccl_speculative_stop(k, monkeypatch):
         for key in G.STATE_KEYS:
             np.testing.assert_array_equal(getattr(got, key), getattr(ref, key), err_msg=key)
         assert e.run(20)[0] == 0
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("k", [5, 30])
+def test_single_rank_rccl_deferred_stop_in_run_timed(k):
+    # the instrumented replay runs the same deferred sequences: a stop inside
+    # one is recovered the same way
+    from gqmap_opticalflow_amd import Engine, comm_unique_id
+    I1, I2, o = _problem("mixture", 1)
+    init, _, tr = _whole(I1, I2, o, "mixture", "fp64", 60, seed=1)
+    tor = float(tr[k, 1]) * (1 + 1e-12)
+    k = int(np.argmax(tr[:, 1] < tor))
+    o = dict(o, tor=tor)
+    _, ref, _ = _whole(I1, I2, o, "mixture", "fp64", 60, seed=1)
+    e = Engine(o, I1, I2, n_tiles=1, tile=0)
+    try:
+        e.attach_rccl(comm_unique_id())
+        e.set_state(init.copy())
+        done, _, _ = e.run_timed(60)
+        assert done == k + 1 and e.info().stopped == 1
+        got = e.get_state()
+        for key in G.STATE_KEYS:
+            np.testing.assert_array_equal(getattr(got, key), getattr(ref, key), err_msg=key)
     finally:
         e.close()

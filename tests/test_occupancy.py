@@ -22,6 +22,11 @@ LIMITS = {
     "_ZN2gq6k_iterIdfLi0ELi1ELb1EEEvNS_10IterParamsIT_T0_EE": 168,
     "_ZN2gq6k_iterIffLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE": 128,
     "_ZN2gq6k_iterIdfLi2ELi1ELb0EEEvNS_10IterParamsIT_T0_EE": 168,
+    # the non-temporal-store variants the large frames run by default (state
+    # > 32 MiB: C5, the full ctf levels of large pyramids)
+    "_ZN2gq6k_iterIdfLi2ELi1ELb1EEEvNS_10IterParamsIT_T0_EE": 168,
+    "_ZN2gq6k_iterIddLi2ELi1ELb1EEEvNS_10IterParamsIT_T0_EE": 168,
+    "_ZN2gq6k_iterIddLi0ELi1ELb1EEEvNS_10IterParamsIT_T0_EE": 168,
     "_ZN2gq6k_iterIddLi2ELi2ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
     "_ZN2gq6k_iterIdfLi1ELi4ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
 }
