@@ -1561,24 +1561,25 @@ __global__ __launch_bounds__(256) void k_seq_snap(const Ctl *ctl, const R *st0, 
 __global__ __launch_bounds__(256) void k_finalize_seq(FinParams F, const fix128 *rows, int n)
 {
     Ctl *ctl = F.ctl;
-    const int NP = NFIX + F.L, tid = threadIdx.x;
-    __shared__ double tot[NFIX + GQMAP_LMAX];
-    __shared__ int stopped;
+    const int NP = NFIX + F.L;
+    // every row's exact totals at once (n NP sums over the ranks), then the
+    // rows applied in iteration order by one thread
+    __shared__ double tot[GRAPH_CHUNK][NFIX + GQMAP_LMAX];
+    if (ctl->stop) return;
+    for (int t = threadIdx.x; t < n * NP; t += blockDim.x) {
+        const int i = t / NP, q = t - i * NP;
+        fix128 v = 0;
+        for (int r = 0; r < F.nranks; ++r) v += rows[((int64_t)r * n + i) * NP + q];
+        tot[i][q] = from_fix(v);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     for (int i = 0; i < n; ++i) {
-        if (tid == 0) stopped = ctl->stop;
-        __syncthreads();
-        if (stopped) return;
-        if (tid < NP) {
-            fix128 v = 0;
-            for (int r = 0; r < F.nranks; ++r) v += rows[((int64_t)r * n + i) * NP + tid];
-            tot[tid] = from_fix(v);
+        fin_apply(F, tot[i]);
+        if (ctl->stop) {
+            if (i < n - 1) ctl->ovr = i + 1;
+            return;
         }
-        __syncthreads();
-        if (tid == 0) {
-            fin_apply(F, tot);
-            if (ctl->stop && i < n - 1) ctl->ovr = i + 1;
-        }
-        __syncthreads();
     }
 }
 

@@ -1,0 +1,34 @@
+"""Profiling driver for one small grid (no torch): C3's middle pyramid levels
+(Grove3 resized, ctf K=11, the library's default lanes per node) or one
+rank's share of the 8-way strong-scaling layout (RubberWhale 388 x 75,
+mixture K=9, Q=4, as a plain fused context).  Runs `its` iterations as
+replayed graphs after a warm-up.  usage: level_prof.py l240|l120|strip8 [its] [fp64|fp32]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from bench import gt_options  # noqa: E402
+from gqmap_opticalflow_amd import Engine, ctf_options, imresize, strip_split  # noqa: E402
+
+case = sys.argv[1] if len(sys.argv) > 1 else "l240"
+its = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+prec = sys.argv[3] if len(sys.argv) > 3 else "fp64"
+if case in ("l240", "l120"):
+    I1, I2, flo, unk, o = gt_options("Grove3", 1, 11)
+    s = 0.5 if case == "l240" else 0.25
+    a, b = (np.asfortranarray(imresize(x, s)) for x in (I1, I2))
+    opts = ctf_options(its=500, minu=o["minu"], maxu=o["maxu"], minv=o["minv"], maxv=o["maxv"])
+    eng = Engine(opts, a, b, "ctf", prec)
+else:
+    I1, I2, flo, unk, o = gt_options("rubberwhale", 1, 9)
+    w = -(-I1.shape[1] // 8) + 2
+    a, b = (np.asfortranarray(x[:, :w]) for x in (I1, I2))
+    eng = Engine(dict(o, split=strip_split(I1.shape[0], I1.shape[1], 8)), a, b, "mixture", prec)
+with eng:
+    eng.init_state(0)
+    eng.run(100)
+    eng.init_state(0)
+    done, tot, ker = eng.run_timed(its)
+    print(f"{case} {a.shape[0]}x{a.shape[1]} {prec} Q={eng.info().split}: k_iter {ker / done * 1e3:.1f} us/it")

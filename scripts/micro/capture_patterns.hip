@@ -24,6 +24,13 @@
 //                capture node when C waits on it
 //   7 stale      per iteration: A k, record e1, k, record e1b; C waits e1 (no
 //                longer A's last node, and not an ancestor of C's)
+//   8 banded-b3  pattern 3 with B = 3 bands
+//   9 banded-ord pattern 3 with the two-iterations-back waits issued before
+//                the neighbour waits
+//  10 banded-anc pattern 2 plus only the two-iterations-back waits on bands
+//                at distance 2 (already ancestors through a neighbour)
+//  11 banded-far pattern 2 plus only the two-iterations-back waits on bands
+//                at distance >= 3 (not ancestors)
 //
 // usage: capture_patterns PATTERN ITERATIONS ; prints "pattern P n N: ok" or
 // the failing call.  Build: hipcc --offload-arch=gfx950 -O2 -o
@@ -72,26 +79,35 @@ int main(int argc, char **argv)
             k_touch<<<1, 64, 0, main_s>>>(cnt, node++);
             CK(hipStreamWaitEvent(main_s, side, 0));
         }
-    } else if (pat >= 1 && pat <= 3) {
+    } else if ((pat >= 1 && pat <= 3) || (pat >= 8 && pat <= 11)) {
         hipEvent_t fork = ev[0];
-        auto bev = [&](int j, int b) { return pat == 3 ? ev[4 + (size_t)j * B + b] : ev[4 + (size_t)(j % 3) * B + b]; };
+        const int NB = pat == 8 ? 3 : B;
+        const bool uniq = pat == 3 || pat >= 8;
+        auto bev = [&](int j, int b) { return uniq ? ev[4 + (size_t)j * B + b] : ev[4 + (size_t)(j % 3) * B + b]; };
+        auto back = [&](int j, int b) {  // the two-iterations-back waits
+            if (j <= 1 || pat == 2) return;
+            for (int b2 = 0; b2 < NB; ++b2) {
+                const int d = b2 > b ? b2 - b : b - b2;
+                if (d <= 1 || (pat == 10 && d != 2) || (pat == 11 && d < 3)) continue;
+                if (hipStreamWaitEvent(st[b], bev(j - 2, b2), 0) != hipSuccess) { printf("wait failed\n"); exit(1); }
+            }
+        };
         k_touch<<<1, 64, 0, main_s>>>(cnt, node++);
         CK(hipEventRecord(fork, main_s));
-        for (int b = 0; b < B; ++b) CK(hipStreamWaitEvent(st[b], fork, 0));
+        for (int b = 0; b < NB; ++b) CK(hipStreamWaitEvent(st[b], fork, 0));
         for (int j = 0; j < n; ++j) {
-            for (int b = 0; b < B; ++b) {
+            for (int b = 0; b < NB; ++b) {
+                if (pat == 9) back(j, b);
                 if (j > 0) {
                     if (b > 0) CK(hipStreamWaitEvent(st[b], bev(j - 1, b - 1), 0));
-                    if (b + 1 < B) CK(hipStreamWaitEvent(st[b], bev(j - 1, b + 1), 0));
+                    if (b + 1 < NB) CK(hipStreamWaitEvent(st[b], bev(j - 1, b + 1), 0));
                 }
-                if (j > 1 && pat != 2)
-                    for (int b2 = 0; b2 < B; ++b2)
-                        if (b2 < b - 1 || b2 > b + 1) CK(hipStreamWaitEvent(st[b], bev(j - 2, b2), 0));
+                if (pat != 9) back(j, b);
                 k_touch<<<1, 64, 0, st[b]>>>(cnt, node++);
                 CK(hipEventRecord(bev(j, b), st[b]));
             }
         }
-        for (int b = 0; b < B; ++b) CK(hipStreamWaitEvent(main_s, bev(n - 1, b), 0));
+        for (int b = 0; b < NB; ++b) CK(hipStreamWaitEvent(main_s, bev(n - 1, b), 0));
     } else if (pat == 4) {
         hipEvent_t fork = ev[0], e = ev[1];
         for (int j = 0; j < n; ++j) {
@@ -139,10 +155,13 @@ int main(int argc, char **argv)
             if (pat == 6) CK(hipStreamWaitEvent(main_s, e2, 0));
         }
     }
+    fprintf(stderr, "pattern %d n %d: calls issued\n", pat, n);
     hipGraph_t g;
     CK(hipStreamEndCapture(main_s, &g));
+    fprintf(stderr, "pattern %d n %d: capture ended\n", pat, n);
     hipGraphExec_t ge;
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    fprintf(stderr, "pattern %d n %d: instantiated\n", pat, n);
     for (int rep = 0; rep < 3; ++rep) CK(hipGraphLaunch(ge, main_s));
     CK(hipStreamSynchronize(main_s));
     std::vector<unsigned> h(nodes);
