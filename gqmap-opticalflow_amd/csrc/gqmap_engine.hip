@@ -2536,13 +2536,19 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
 // Deferred-totals RCCL step (L = 1).  Nothing of iteration j + 1 depends on
 // iteration j's totals but the stop rule (alpha is constant, the step size
 // and the temperature decay follow the iteration number), so the totals'
-// all-gather and the finalize leave the iteration: per iteration only
-//   main  fork | interior k_iter               | wait exchange | unpack + advance
-//   side        boundary k_iter, pack, send/recv | (ev_xch)
+// all-gather and the finalize leave the iteration, and everything of an
+// iteration runs on the context's one stream:
+//   k_iter (all the strip's tiles) | pack | send/recv | unpack + advance
 // with this tile's exact totals of iteration pos written to row pos of
-// d_rows by the last workgroup of the two k_iter launches, and the kernels
-// running by Ctl::it_i / done_i / T_i (k_unpack_advance takes fin_apply's
-// steps for them).  A sequence of n <= GRAPH_CHUNK iterations
+// d_rows by the launch's last workgroup, and the kernels running by
+// Ctl::it_i / done_i / T_i (k_unpack_advance takes fin_apply's steps for
+// them).  No cross-stream edge: on MI355X each one cost 5-10 us per
+// iteration (profiles/r05_strip8_timeline.txt: the round-4 boundary/interior
+// split on two streams ran a one-rank 8-way strip at 63 us/it under the
+// profiler, 20 us over the kernel; with neighbours it would have overlapped
+// the boundary columns' exchange with the interior tiles, which the
+// cross-queue edges cost as much as they saved).  A sequence of
+// n <= GRAPH_CHUNK iterations
 //   k_seq_snap (state + Ctl, unless stopped) | n iterations |
 //   one all-gather of the n rows | k_finalize_seq (fin_apply per row: the
 //   trace, it / done / T, the stop rule)
@@ -2551,9 +2557,7 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
 // later sequences turn into no-ops (Ctl::stop), and the host restores the
 // snapshot and re-runs the i + 1 iterations with the exact per-iteration
 // step (deferred_recover) -- the same state, trace and stop iteration as the
-// whole grid.  Every stream capture below records an event and has it waited
-// on before the event is recorded again (the pattern of launch_step_rccl;
-// DESIGN.md 5 on HIP's capture).
+// whole grid.
 // (the snapshot buffers are allocated outside any capture -- gqmap_tile_attach_rccl,
 // capture_steps -- and follow the grid size; without them the exact step runs)
 bool deferred(const gqmap_ctx *c)
@@ -2574,8 +2578,8 @@ void unpack_advance_t(gqmap_ctx *c)
                                                   c->opt.t_decay_every, c->opt.drate, c->opt.t_min);
 }
 
-// Iteration `pos` of a deferred sequence; e0 / e1 (optional) bracket the two
-// k_iter launches.
+// Iteration `pos` of a deferred sequence; e0 / e1 (optional) bracket its
+// k_iter launch.
 gqmap_status launch_step_deferred(gqmap_ctx *c, int pos, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
     const int r = c->comm->rank;
@@ -2583,38 +2587,32 @@ gqmap_status launch_step_deferred(gqmap_ctx *c, int pos, hipEvent_t e0 = nullptr
     const size_t nl = (size_t)HALO_TO_LEFT_N * c->L * c->M, nr = (size_t)HALO_TO_RIGHT_N * c->L * c->M;
     const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
     const Rccl *R = rccl();
-    TileSegs bnd, inr;
+    // every tile column from the one holding the first owned column (a
+    // ghost-only tile column -- one-column tiles of a strip with a left
+    // neighbour -- is not launched): the blocks iteration_blocks() counts
+    TileSegs bnd, inr, all{};
     tile_segments(c, bnd, inr);
+    all.lo[0] = bnd.lo[0];
+    all.n[0] = c->tiles_m * c->tiles_n - bnd.lo[0];
+    all.part_off = 0;
     c->spec_now = true;
     c->seq_row = c->d_rows + (size_t)pos * (NFIX + c->L);
-    hipStream_t main_stream = c->stream;
-    if (e0) GQ_HIP(hipEventRecord(e0, main_stream));
-    GQ_HIP(hipEventRecord(c->ev_fork, main_stream));
-    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    c->stream = c->side;
-    launch_iter(c, &bnd);
-    c->stream = main_stream;
-    GQ_HIP(hipEventRecord(c->ev_bnd, c->side));
-    halo_pack(c, c->side);
+    if (e0) GQ_HIP(hipEventRecord(e0, c->stream));
+    launch_iter(c, &all);
+    if (e1) GQ_HIP(hipEventRecord(e1, c->stream));
     if (left || right) {
+        halo_pack(c, c->stream);
         GQ_NCCL(R->GroupStart());
         if (left) {
-            GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->side));
-            GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->side));
+            GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->stream));
+            GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->stream));
         }
         if (right) {
-            GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->side));
-            GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->side));
+            GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->stream));
+            GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->stream));
         }
         GQ_NCCL(R->GroupEnd());
     }
-    GQ_HIP(hipEventRecord(c->ev_xch, c->side));
-    launch_iter(c, &inr);
-    if (e1) {
-        GQ_HIP(hipStreamWaitEvent(main_stream, c->ev_bnd, 0));
-        GQ_HIP(hipEventRecord(e1, main_stream));
-    }
-    GQ_HIP(hipStreamWaitEvent(main_stream, c->ev_xch, 0));
     if (c->fp32) unpack_advance_t<float>(c);
     else unpack_advance_t<double>(c);
     c->spec_now = false;
