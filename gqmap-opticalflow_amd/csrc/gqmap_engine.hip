@@ -1872,10 +1872,6 @@ struct gqmap_ctx {
     struct RcclComm *comm = nullptr;
     bool in_group = false;
     bool host_xfer = false;  // gqmap_tile_attach_host: the caller moves the data
-    // RCCL tiles: the ghost-column exchange runs on `side` while the interior
-    // tiles run on `stream` (fork / join events)
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_bnd = nullptr, ev_inr = nullptr, ev_xch = nullptr;
     // deferred-totals RCCL step (L = 1, launch_seq_deferred): each iteration
     // of a sequence writes this tile's exact totals to row `pos` of d_rows; the
     // sequence ends with one all-gather of its rows into d_seqg
@@ -2478,57 +2474,64 @@ gqmap_status launch_tail(gqmap_ctx *c)
     return GQMAP_OK;
 }
 
-// One iteration of an RCCL tile.  The boundary tile columns run first; their
-// owned edge columns are packed and sent to the neighbour ranks (grouped
-// ncclSend/ncclRecv over xGMI) on the side stream while the interior tiles
-// run on the context's stream.  Then this tile's exact totals, their
-// all-gather, the received columns into the ghost columns, and the finalize
-// over all tiles' totals (identical on every rank).  e0 / e1 (optional)
-// bracket the two k_iter launches on the main stream.
-gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
+// The strip's tiles of one RCCL iteration as one launch: every tile column
+// from the one holding the first owned column (a ghost-only tile column --
+// one-column tiles of a strip with a left neighbour -- is not launched; the
+// workgroups iteration_blocks() counts).
+TileSegs strip_launch(const gqmap_ctx *c)
 {
-    const int NP = NFIX + c->L, r = c->comm->rank;
+    TileSegs bnd, inr, all{};
+    tile_segments(c, bnd, inr);
+    all.lo[0] = bnd.lo[0];
+    all.n[0] = c->tiles_m * c->tiles_n - bnd.lo[0];
+    all.part_off = 0;
+    return all;
+}
+
+// The ghost-column exchange of an iteration on the context stream: pack the
+// boundary columns, grouped ncclSend/ncclRecv with the neighbour ranks.
+gqmap_status exchange_rccl(gqmap_ctx *c)
+{
+    const int r = c->comm->rank;
     const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
+    if (!left && !right) return GQMAP_OK;
     const size_t nl = (size_t)HALO_TO_LEFT_N * c->L * c->M, nr = (size_t)HALO_TO_RIGHT_N * c->L * c->M;
     const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
     const Rccl *R = rccl();
-    TileSegs bnd, inr;
-    tile_segments(c, bnd, inr);
-    if (e0) GQ_HIP(hipEventRecord(e0, c->stream));
-    // the boundary tile columns on the side stream, at the same time as the
-    // interior tiles on the main stream (a strip's boundary launch alone
-    // holds few workgroups: run back to back the two launches cost two tile
-    // latencies per iteration); their owned columns are packed and
-    // exchanged as soon as they are done
-    GQ_HIP(hipEventRecord(c->ev_fork, c->stream));
-    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    hipStream_t main_stream = c->stream;
-    c->stream = c->side;
-    launch_iter(c, &bnd);
-    c->stream = main_stream;
-    GQ_HIP(hipEventRecord(c->ev_bnd, c->side));
-    halo_pack(c, c->side);
+    halo_pack(c, c->stream);
     GQ_NCCL(R->GroupStart());
     if (left) {
-        GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->side));
-        GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->side));
+        GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->stream));
+        GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->stream));
     }
     if (right) {
-        GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->side));
-        GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->side));
+        GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->stream));
+        GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->stream));
     }
     GQ_NCCL(R->GroupEnd());
-    launch_iter(c, &inr);
-    GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_bnd, 0));  // both launches' partial rows
+    return GQMAP_OK;
+}
+
+// One exact iteration of an RCCL tile (L > 1, whose alpha update needs every
+// iteration's totals; and the re-run of a deferred sequence that overshot its
+// stop): the strip's tiles, the exchange, this tile's exact totals
+// all-gathered, then the received columns into the ghost columns and the
+// finalize over all tiles' totals (identical on every rank) -- all on the
+// context's stream (a cross-stream edge costs 5-10 us per iteration here,
+// profiles/r05_strip8_timeline.txt).  e0 / e1 (optional) bracket the k_iter
+// launch.
+gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
+{
+    const int NP = NFIX + c->L, r = c->comm->rank;
+    const TileSegs all = strip_launch(c);
+    if (e0) GQ_HIP(hipEventRecord(e0, c->stream));
+    launch_iter(c, &all);
     if (e1) GQ_HIP(hipEventRecord(e1, c->stream));
-    // (this rank's totals row was written by the last workgroup of the two
-    // launches: tile_totals_tail)
-    GQ_HIP(hipEventRecord(c->ev_inr, c->stream));
-    GQ_HIP(hipStreamWaitEvent(c->side, c->ev_inr, 0));
-    GQ_NCCL(R->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
-                         c->comm->comm, c->side));
-    GQ_HIP(hipEventRecord(c->ev_xch, c->side));
-    GQ_HIP(hipStreamWaitEvent(c->stream, c->ev_xch, 0));
+    gqmap_status st = exchange_rccl(c);
+    if (st != GQMAP_OK) return st;
+    // (this rank's totals row was written by the launch's last workgroup: tile_totals_tail)
+    GQ_NCCL(rccl()->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
+                              c->comm->comm, c->stream));
     unpack_finalize(c);  // received ghost columns + finalize, one launch
     return GQMAP_OK;
 }
@@ -2582,42 +2585,20 @@ void unpack_advance_t(gqmap_ctx *c)
 // k_iter launch.
 gqmap_status launch_step_deferred(gqmap_ctx *c, int pos, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr)
 {
-    const int r = c->comm->rank;
-    const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
-    const size_t nl = (size_t)HALO_TO_LEFT_N * c->L * c->M, nr = (size_t)HALO_TO_RIGHT_N * c->L * c->M;
-    const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
-    const Rccl *R = rccl();
-    // every tile column from the one holding the first owned column (a
-    // ghost-only tile column -- one-column tiles of a strip with a left
-    // neighbour -- is not launched): the blocks iteration_blocks() counts
-    TileSegs bnd, inr, all{};
-    tile_segments(c, bnd, inr);
-    all.lo[0] = bnd.lo[0];
-    all.n[0] = c->tiles_m * c->tiles_n - bnd.lo[0];
-    all.part_off = 0;
+    const TileSegs all = strip_launch(c);
     c->spec_now = true;
     c->seq_row = c->d_rows + (size_t)pos * (NFIX + c->L);
     if (e0) GQ_HIP(hipEventRecord(e0, c->stream));
     launch_iter(c, &all);
     if (e1) GQ_HIP(hipEventRecord(e1, c->stream));
-    if (left || right) {
-        halo_pack(c, c->stream);
-        GQ_NCCL(R->GroupStart());
-        if (left) {
-            GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->stream));
-            GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->stream));
-        }
-        if (right) {
-            GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->stream));
-            GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->stream));
-        }
-        GQ_NCCL(R->GroupEnd());
+    gqmap_status st = exchange_rccl(c);
+    if (st == GQMAP_OK) {
+        if (c->fp32) unpack_advance_t<float>(c);
+        else unpack_advance_t<double>(c);
     }
-    if (c->fp32) unpack_advance_t<float>(c);
-    else unpack_advance_t<double>(c);
     c->spec_now = false;
     c->seq_row = nullptr;
-    return GQMAP_OK;
+    return st;
 }
 
 // A deferred sequence of n (1..GRAPH_CHUNK) iterations; ev (optional): 2 n
@@ -3774,9 +3755,6 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
     c->comm = cm;
     gqmap_status s = attach_common(c);
     if (s != GQMAP_OK) return s;
-    GQ_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    for (hipEvent_t *e : {&c->ev_fork, &c->ev_bnd, &c->ev_inr, &c->ev_xch})
-        GQ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     if (c->L == 1) {  // deferred-totals sequences (launch_seq_deferred)
         const size_t NP = NFIX + c->L;
         GQ_HIP(hipMalloc((void **)&c->d_rows, sizeof(fix128) * NP * GRAPH_CHUNK));
@@ -3960,10 +3938,6 @@ void gqmap_destroy(gqmap_ctx *c)
         (void)rccl()->CommDestroy(c->comm->comm);
         delete c->comm;
     }
-    if (c->side) (void)hipStreamSynchronize(c->side);
-    for (hipEvent_t e : {c->ev_fork, c->ev_bnd, c->ev_inr, c->ev_xch})
-        if (e) (void)hipEventDestroy(e);
-    if (c->side) (void)hipStreamDestroy(c->side);
     for (void *p : {(void *)c->d_rows, (void *)c->d_seqg})
         if (p) (void)hipFree(p);
     if (c->own_gathered && c->d_gathered) (void)hipFree(c->d_gathered);

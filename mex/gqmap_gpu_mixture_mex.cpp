@@ -91,6 +91,11 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[])
     // optional (not read by the reference): projsplx alpha update (:49 / super :48, commented there)
     if (mxGetField(opt, 0, "alpha_mode"))
         fail(gqmap_options_alpha_mode(&o, (int)field_d(opt, "alpha_mode")), "options.alpha_mode");
+    // optional (not read by the reference): options.arith = 'literal' runs the
+    // reference's own operation order (GQMAP_ARITH_LITERAL: bit-identical to a
+    // literal fp64 restatement of the MATLAB; fp64 mixture engine)
+    if (mxGetField(opt, 0, "arith"))
+        o.arith = field_s(opt, "arith") == "literal" ? GQMAP_ARITH_LITERAL : GQMAP_ARITH_FAST;
     const uint64_t seed = (uint64_t)field_d(opt, "seed", false, 0);
     const std::string dir = field_s(opt, "dir");
     const mxArray *tflow = mxGetField(opt, 0, "trueFlow");
