@@ -14,9 +14,11 @@ for r in rows:
         segs.append(cur)
         cur = []
     elif "k_iter" in n:
-        cur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        kind = "k_iter_lit" if "k_iter_lit" in n else "k_iter"
+        cur.append((kind, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
 segs.append(cur)
-print(f"{'segment':>7s} {'launches':>8s} {'mean_us':>8s} {'min_us':>7s} {'max_us':>7s}")
+print(f"{'segment':>7s} {'kernel':>10s} {'launches':>8s} {'mean_us':>8s} {'min_us':>7s} {'max_us':>7s}")
 for i, s in enumerate(segs):
     if s:
-        print(f"{i:7d} {len(s):8d} {sum(s) / len(s):8.1f} {min(s):7.1f} {max(s):7.1f}")
+        d = [x for _, x in s]
+        print(f"{i:7d} {s[0][0]:>10s} {len(d):8d} {sum(d) / len(d):8.1f} {min(d):7.1f} {max(d):7.1f}")
