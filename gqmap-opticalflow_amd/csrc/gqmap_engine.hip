@@ -3355,12 +3355,19 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
                 GQ_HIP(hipGraphLaunch(c->graph, c->stream));
                 left -= GRAPH_CHUNK;
             }
-            for (int k = SUB_GRAPHS - 1; k >= 0; --k)
-                if (left & (1 << k)) {
-                    if ((s = ensure_sub_graph(c, k)) != GQMAP_OK) return s;
-                    GQ_HIP(hipGraphLaunch(c->sub[k], c->stream));
-                }
-            left = 0;
+            // (a persistent small-level context or a deferred RCCL strip runs
+            // the remainder as ONE launch / one sequence, directly: as 2^k
+            // graphs it would pay a snapshot and a grid-barrier start-up, or
+            // a snapshot, an all-gather and a finalize, per sub-graph)
+            const bool one = left > 0 && (deferred(c) || launch_persist(c, left, true));
+            if (!one) {
+                for (int k = SUB_GRAPHS - 1; k >= 0; --k)
+                    if (left & (1 << k)) {
+                        if ((s = ensure_sub_graph(c, k)) != GQMAP_OK) return s;
+                        GQ_HIP(hipGraphLaunch(c->sub[k], c->stream));
+                    }
+                left = 0;
+            }
         }
         if (left > 0 && (s = launch_steps(c, left)) != GQMAP_OK) return s;
         GQ_HIP(hipGetLastError());

@@ -7,6 +7,10 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _policy  # noqa: E402
+
+_policy.apply()
 import numpy as np  # noqa: E402
 
 from bench import gt_options  # noqa: E402

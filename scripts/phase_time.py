@@ -5,6 +5,10 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _policy  # noqa: E402
+
+_policy.apply()
 from bench import gt_options, setup_problem  # noqa: E402
 from gqmap_opticalflow_amd import Engine  # noqa: E402
 
