@@ -195,7 +195,7 @@ struct IterParams {
     int guard;
     int64_t MNL;
     unsigned *bar;  // k_iter_persist: barrier counters (BAR_WORDS, zero between launches)
-    int spec;       // speculative RCCL tile: run iteration Ctl::it_i / done_i / T_i
+    int spec;       // deferred-totals RCCL tile: run iteration Ctl::it_i / done_i / T_i
 };
 
 // Quadrature tables are read with wave-uniform indices; routing them through
@@ -768,8 +768,8 @@ __device__ __forceinline__ void fused_finalize_tail(const FinParams &F)
     }
 }
 
-// RCCL tile: the last of the iteration's ticket_total workgroups (both the
-// boundary and the interior launch) turns Ctl::acc into the tile's exact
+// RCCL tile: the last of the iteration's ticket_total workgroups (the
+// strip's launch) turns Ctl::acc into the tile's exact
 // totals (fix128, this rank's row of the table the all-gather shares) and
 // clears acc and the ticket.  All threads of every workgroup call it.
 __device__ __forceinline__ void tile_totals_tail(const FinParams &F, int total, fix128 *out)
@@ -1680,18 +1680,18 @@ __global__ __launch_bounds__(256) void k_unpack_finalize(FinParams F, R *st0, R 
     fin_reduce(F, tot, sh);  // (its barriers order every thread's parity read before fin_apply)
     if (threadIdx.x == 0) {
         fin_apply(F, tot);
-        ctl->it_i = ctl->it;  // the speculative counters follow (a later spec run starts here)
+        ctl->it_i = ctl->it;  // the kernels' counters follow (a later deferred sequence starts here)
         ctl->done_i = ctl->done;
         ctl->T_i = ctl->T;
     }
 }
 
-// Speculative RCCL tile (L = 1): the received ghost columns into the state
+// Deferred-totals RCCL tile (L = 1): the received ghost columns into the state
 // buffer the iteration just wrote, then the iteration counters the kernels
 // run by -- the same steps fin_apply takes (temperature decay after
 // iteration it_i, it + 1, done + 1), without waiting for the totals: nothing
 // of the next iteration depends on them but the stop rule, which the
-// finalize (k_finalize, on its own stream) judges one iteration behind.
+// sequence's finalize (k_finalize_seq) judges at the end of the sequence.
 template <typename R>
 __global__ __launch_bounds__(256) void k_unpack_advance(Ctl *ctl, R *st0, R *st1, int M, int64_t MN, int64_t MNL,
                                                         int L, HaloSide<R> s0, HaloSide<R> s1, int nsides,
@@ -3487,7 +3487,7 @@ gqmap_status gqmap_prepare(gqmap_ctx *c)
 // Not in the public header (tests, no device needed): the launch geometry of
 // column-strip tile `tile` of n_tiles over a Mo x No frame -- out = {nblocks
 // (the whole local tile grid), iteration_blocks (the workgroups of one RCCL
-// iteration: boundary + interior launches), tiles_m, tiles_n, kernel shape}.
+// iteration: the strip's launch), tiles_m, tiles_n, kernel shape}.
 int gqmap_debug_strip_launch(const gqmap_options *opt, int Mo, int No, int n_tiles, int tile, int out[5])
 {
     if (!opt || !out || n_tiles < 1 || tile < 0 || tile >= n_tiles) return GQMAP_ERR_INVALID_ARG;
@@ -3716,9 +3716,8 @@ gqmap_status gqmap_create_tile(gqmap_ctx **out, const gqmap_options *opt, int de
 static gqmap_status attach_common(gqmap_ctx *c)
 {
     const size_t NP = NFIX + c->L;
-    // two halves: the speculative RCCL step alternates them by iteration parity
-    GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles * 2));
-    GQ_HIP(hipMemsetAsync(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles * 2, c->stream));
+    GQ_HIP(hipMalloc((void **)&c->d_gathered, sizeof(fix128) * NP * c->n_tiles));
+    GQ_HIP(hipMemsetAsync(c->d_gathered, 0, sizeof(fix128) * NP * c->n_tiles, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     c->own_gathered = true;
     c->nranks = c->n_tiles;
