@@ -5,11 +5,12 @@
 // shift in the gradient sum (:58-60), plain gradient ascent with
 // sigma = |sigma + dsigma*step| and rou clamped to +-0.97 (:62-65).
 //
-// Per iteration: k_legacy_grad (one thread per node m < M-1, n < N-1: the
-// K-point node rule and the four K x K edge rules, written to dnode/dedge in
-// the reference's M x N x 2 x 2 / M x N x 2 x 5 x 2 layout), k_legacy_update
-// (one thread per node and layer: sums, step, clamps, exact running maxima
-// via atomicMax on the bit patterns of |x|), k_legacy_ctl (trace, stop rule).
+// Per iteration: k_legacy_grad (one thread per node m < M-1, n < N-1, edge
+// and layer: one K x K edge rule, plus the K-point node rule on the j = 0
+// threads, written to dnode/dedge in the reference's M x N x 2 x 2 /
+// M x N x 2 x 5 x 2 layout), k_legacy_update (one thread per node and layer:
+// sums, step, clamps, per-workgroup maxima on the bit patterns of |x|),
+// k_legacy_ctl (their maxima -> trace, stop rule).
 // No host round trip inside the loop.  Plain fp64 with contraction off in the
 // order of the MATLAB expressions, so the device matches the C restatement
 // (oracle/gqmap_legacy_oracle.c) bit for bit.
@@ -31,12 +32,13 @@ constexpr int LG_KMAX = GQMAP_KMAX;
 struct LgParams {
     const double *flow;
     double *mu, *sigma, *rou, *dnode, *dedge;
-    unsigned long long *maxbits;  // [its][3]
+    unsigned long long *blkmax;   // [update workgroups][3]: |dmu|, |dsigma|, |drou| maxima as bits
     int *ctl;                     // it, stop, done
     double *trace;
-    int M, N, K, its, min_its;
+    int M, N, K, its, min_its, nblk;
     double var, gama, dta, step0, step_decay, corr, tor;
     double X[LG_KMAX], W[LG_KMAX];
+    double WW[LG_KMAX * LG_KMAX];  // W[c] * W[r] at r + K*c (WIWJ, :5-6), the host's product
 };
 
 __device__ __forceinline__ size_t i3(int M, int N, int m, int n, int l) { return m + (size_t)M * (n + (size_t)N * l); }
@@ -49,21 +51,41 @@ __device__ __forceinline__ size_t i5(int M, int N, int m, int n, int j, int q, i
     return m + (size_t)M * (n + (size_t)N * (j + 2 * (q + 5 * (size_t)l)));
 }
 
-// GAMA1 / VAR1: gama == 1 / var == 1, where x / 1 == x exactly (no division)
-template <bool GAMA1, bool VAR1>
-__global__ void k_legacy_grad(LgParams P)
+// One thread per node m < M-1, n < N-1, edge j and layer l ((j, l) slowest:
+// a wave stays on one edge of one layer): the edge rule (j, l) of the node,
+// and on the j = 0 threads the node rule of layer l too (9 of ~170 points).
+// Every expression keeps the reference's operand order; what is hoisted is a
+// whole subexpression of it, computed once with the same operands:
+//   s*XI, t*XI, ds*XI, dt*XI per column c and t*XJ, s*XJ, dt*XJ, ds*XJ per
+//   row r (when K is a template constant: held in registers), sq2*o1 and
+//   sq2*o2, WIWJ from the host table.
+// c2 (the sum of df2 = -df1) is 0 - c1 exactly: both start at +0, IEEE
+// addition is symmetric under negation, and an exact-zero sum is +0 in both
+// chains -- so column and total sums of df2 are not formed (s2 = 0 - s1).
+// KT: K as a template constant (0: P.K at run time); GAMA1 / VAR1: gama == 1
+// / var == 1, where x / 1 == x exactly; DTA_INF: dta == inf, where
+// fabs(diff) > dta is false for every diff (NaN included).
+template <int KT, bool GAMA1, bool VAR1, bool DTA_INF>
+__global__ __launch_bounds__(256) void k_legacy_grad(LgParams P)
 {
     if (P.ctl[1]) return;
-    const int M = P.M, N = P.N, K = P.K;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (int64_t)(M - 1) * (N - 1)) return;
+    const int M = P.M, N = P.N, K = KT ? KT : P.K;
+    constexpr int UNR = KT ? KT : 1;  // full unroll for a constant K
+    const int64_t MN1 = (int64_t)(M - 1) * (N - 1);
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 4 * MN1) return;
+    const int jl = (int)(t / MN1), j = jl & 1, l = jl >> 1;
+    t -= jl * MN1;
     const int m = (int)(t % (M - 1)), n = (int)(t / (M - 1));
     const double sq2 = sqrt(2.0), PI = 3.14159265358979323846;
-    for (int l = 0; l < 2; ++l) {  // (:20-26)
-        const double o = P.sigma[i3(M, N, m, n, l)], u = P.mu[i3(M, N, m, n, l)], f = P.flow[i3(M, N, m, n, l)];
+    const double o1 = P.sigma[i3(M, N, m, n, l)], u1 = P.mu[i3(M, N, m, n, l)];
+    const double so1 = sq2 * o1;
+    if (j == 0) {  // (:20-26)
+        const double f = P.flow[i3(M, N, m, n, l)];
         double du = 0, dsum = 0;
+#pragma unroll UNR
         for (int k = 0; k < K; ++k) {
-            const double x = sq2 * o * P.X[k] + u;
+            const double x = so1 * P.X[k] + u1;
             const double dval = VAR1 ? P.W[k] * (f - x) : P.W[k] * (f - x) / P.var;
             du += dval;
             dsum += dval * P.X[k];
@@ -71,40 +93,54 @@ __global__ void k_legacy_grad(LgParams P)
         P.dnode[i4(M, N, m, n, 0, l)] = du / sqrt(PI);
         P.dnode[i4(M, N, m, n, 1, l)] = dsum * sqrt(2.0 / PI);
     }
-    for (int j = 0; j < 2; ++j) {  // (:28-54)
+    {  // (:28-54)
         const int m2 = m + (j == 0), n2 = n + (j == 1);
-        for (int l = 0; l < 2; ++l) {
-            const double p = P.rou[i4(M, N, m, n, j, l)];
-            const double o1 = P.sigma[i3(M, N, m, n, l)], o2 = P.sigma[i3(M, N, m2, n2, l)];
-            const double u1 = P.mu[i3(M, N, m, n, l)], u2 = P.mu[i3(M, N, m2, n2, l)];
-            const double q = sqrt(1 + p), r = sqrt(1 - p);
-            const double s = (q + r) / 2, tt = (q - r) / 2;
-            const double ds = (1 / q - 1 / r) / 4, dt = (1 / q + 1 / r) / 4;
-            double s1 = 0, s2 = 0, so1 = 0, so2 = 0, sp = 0;
-            for (int c = 0; c < K; ++c) {  // sum(sum(A)): column sums first
-                double c1 = 0, c2 = 0, co1 = 0, co2 = 0, cp = 0;
-                const double xi = P.X[c];
-                for (int rr = 0; rr < K; ++rr) {
-                    const double xj = P.X[rr], ww = P.W[c] * P.W[rr];
-                    const double ZI = s * xi + tt * xj, ZJ = tt * xi + s * xj;
-                    const double x1 = sq2 * o1 * ZI + u1, x2 = sq2 * o2 * ZJ + u2;
-                    double diff = x2 - x1;
-                    if (fabs(diff) > P.dta) diff = 0;  // (:44)
-                    const double df1 = GAMA1 ? ww * diff : ww * diff / P.gama, df2 = -df1;
-                    c1 += df1;
-                    c2 += df2;
-                    co1 += df1 * ZI;
-                    co2 += df2 * ZJ;
-                    cp += o1 * df1 * (ds * xi + dt * xj) + o2 * df2 * (dt * xi + ds * xj);
-                }
-                s1 += c1; s2 += c2; so1 += co1; so2 += co2; sp += cp;
+        const double p = P.rou[i4(M, N, m, n, j, l)];
+        const double o2 = P.sigma[i3(M, N, m2, n2, l)], u2 = P.mu[i3(M, N, m2, n2, l)];
+        const double so2 = sq2 * o2;
+        const double q = sqrt(1 + p), r = sqrt(1 - p);
+        const double s = (q + r) / 2, tt = (q - r) / 2;
+        const double ds = (1 / q - 1 / r) / 4, dt = (1 / q + 1 / r) / 4;
+        double txj[UNR], sxj[UNR], dtxj[UNR], dsxj[UNR];
+        if (KT) {
+#pragma unroll UNR
+            for (int rr = 0; rr < UNR; ++rr) {
+                txj[rr] = tt * P.X[rr];
+                sxj[rr] = s * P.X[rr];
+                dtxj[rr] = dt * P.X[rr];
+                dsxj[rr] = ds * P.X[rr];
             }
-            P.dedge[i5(M, N, m, n, j, 0, l)] = 1 / PI * s1;
-            P.dedge[i5(M, N, m, n, j, 1, l)] = 1 / PI * s2;
-            P.dedge[i5(M, N, m, n, j, 2, l)] = 1 / PI * sq2 * so1;
-            P.dedge[i5(M, N, m, n, j, 3, l)] = 1 / PI * sq2 * so2;
-            P.dedge[i5(M, N, m, n, j, 4, l)] = 1 / PI * sq2 * sp;
         }
+        double s1 = 0, so1s = 0, so2s = 0, sp = 0;
+#pragma unroll UNR
+        for (int c = 0; c < K; ++c) {  // sum(sum(A)): column sums first
+            const double xi = P.X[c];
+            const double sxi = s * xi, txi = tt * xi, dsxi = ds * xi, dtxi = dt * xi;
+            double c1 = 0, co1 = 0, co2 = 0, cp = 0;
+#pragma unroll UNR
+            for (int rr = 0; rr < K; ++rr) {
+                const double xj = P.X[rr];
+                const double tx = KT ? txj[rr] : tt * xj, sx = KT ? sxj[rr] : s * xj;
+                const double dtx = KT ? dtxj[rr] : dt * xj, dsx = KT ? dsxj[rr] : ds * xj;
+                const double ZI = sxi + tx, ZJ = txi + sx;
+                const double x1 = so1 * ZI + u1, x2 = so2 * ZJ + u2;
+                double diff = x2 - x1;
+                if (!DTA_INF && fabs(diff) > P.dta) diff = 0;  // (:44)
+                const double ww = P.WW[rr + K * c];
+                const double df1 = GAMA1 ? ww * diff : ww * diff / P.gama, df2 = -df1;
+                c1 += df1;
+                co1 += df1 * ZI;
+                co2 += df2 * ZJ;
+                cp += o1 * df1 * (dsxi + dtx) + o2 * df2 * (dtxi + dsx);
+            }
+            s1 += c1; so1s += co1; so2s += co2; sp += cp;
+        }
+        const double s2 = 0.0 - s1;
+        P.dedge[i5(M, N, m, n, j, 0, l)] = 1 / PI * s1;
+        P.dedge[i5(M, N, m, n, j, 1, l)] = 1 / PI * s2;
+        P.dedge[i5(M, N, m, n, j, 2, l)] = 1 / PI * sq2 * so1s;
+        P.dedge[i5(M, N, m, n, j, 3, l)] = 1 / PI * sq2 * so2s;
+        P.dedge[i5(M, N, m, n, j, 4, l)] = 1 / PI * sq2 * sp;
     }
 }
 
@@ -115,36 +151,39 @@ __device__ __forceinline__ unsigned long long abits(double v)
     return (unsigned long long)__double_as_longlong(fabs(v));
 }
 
-// Block maximum of three bit patterns, then one atomicMax per slot and block
-// (one atomic per thread on three addresses serialised in L2: 240 us/launch).
-__device__ void block_amax3(unsigned long long *slot, unsigned long long a, unsigned long long b,
-                            unsigned long long c)
+// Maximum over the block of three bit patterns (thread 0 holds the result).
+__device__ void block_max3(unsigned long long &a, unsigned long long &b, unsigned long long &c)
 {
-    __shared__ unsigned long long red[3][4];
+    __shared__ unsigned long long red[3][16];
     for (int o = 32; o > 0; o >>= 1) {
         a = max(a, __shfl_xor(a, o));
         b = max(b, __shfl_xor(b, o));
         c = max(c, __shfl_xor(c, o));
     }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = (int)(blockDim.x + 63) >> 6;
     if (lane == 0) { red[0][wave] = a; red[1][wave] = b; red[2][wave] = c; }
     __syncthreads();
-    if (threadIdx.x < 3) {
-        const int q = threadIdx.x;
-        const unsigned long long v = max(max(red[q][0], red[q][1]), max(red[q][2], red[q][3]));
-        if (v) atomicMax(slot + q, v);
-    }
+    if (threadIdx.x == 0)
+        for (int w = 1; w < nw; ++w) {
+            a = max(a, red[0][w]);
+            b = max(b, red[1][w]);
+            c = max(c, red[2][w]);
+        }
 }
 
-__global__ void k_legacy_update(LgParams P)
+// One thread per node and layer: sums, step, clamps; the workgroup's maxima
+// of |dmu|, |dsigma|, |drou| go to its own blkmax row (plain stores: one
+// atomicMax per workgroup on three shared addresses serialises in L2, and a
+// last-workgroup reduction needs a device-scope release per workgroup, an L2
+// writeback each -- 70 us per launch) and k_legacy_ctl reduces the rows.
+__global__ __launch_bounds__(256) void k_legacy_update(LgParams P)
 {
     if (P.ctl[1]) return;
     const int M = P.M, N = P.N;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int it = P.ctl[0];
-    unsigned long long *slot = P.maxbits + 3 * (size_t)(it - 1);
     // Threads past the last node contribute zeros: every thread reaches the
-    // single block_amax3 call below (its barrier is never on a divergent path).
+    // single block_max3 call below (its barrier is never on a divergent path).
     double a = 0, b = 0, mp = 0;
     if (t < (int64_t)M * N * 2) {
         const int m = (int)(t % M), n = (int)((t / M) % N), l = (int)(t / ((int64_t)M * N));
@@ -169,7 +208,14 @@ __global__ void k_legacy_update(LgParams P)
             P.rou[r] = fmax(fmin(P.rou[r] + d * step, P.corr), -P.corr);
         }
     }
-    block_amax3(slot, abits(a), abits(b), abits(mp));
+    unsigned long long ba = abits(a), bb = abits(b), bm = abits(mp);
+    block_max3(ba, bb, bm);
+    if (threadIdx.x == 0) {
+        unsigned long long *row = P.blkmax + 3 * (size_t)blockIdx.x;
+        row[0] = ba;
+        row[1] = bb;
+        row[2] = bm;
+    }
 }
 
 // sigma = rand(M,N,2) + 2 (:10) from the library RNG stream 3: the host
@@ -180,14 +226,25 @@ __global__ void k_legacy_sigma0(double *sigma, int64_t n, uint64_t base)
     if (i < n) sigma[i] = u01(base, (uint64_t)i) + 2;
 }
 
-__global__ void k_legacy_ctl(LgParams P)
+// One workgroup: the maxima over the update's blkmax rows -> trace, then
+// the iteration counter and the stop rule.
+__global__ __launch_bounds__(1024) void k_legacy_ctl(LgParams P)
 {
     if (P.ctl[1]) return;
+    unsigned long long a = 0, b = 0, c = 0;
+    for (int i = threadIdx.x; i < P.nblk; i += blockDim.x) {
+        const unsigned long long *row = P.blkmax + 3 * (size_t)i;
+        a = max(a, row[0]);
+        b = max(b, row[1]);
+        c = max(c, row[2]);
+    }
+    block_max3(a, b, c);
+    if (threadIdx.x != 0) return;
     const int it = P.ctl[0];
-    const unsigned long long *slot = P.maxbits + 3 * (size_t)(it - 1);
+    const unsigned long long bits[3] = {a, b, c};
     double mx[3];
     for (int q = 0; q < 3; ++q) {
-        mx[q] = __longlong_as_double((long long)slot[q]);
+        mx[q] = __longlong_as_double((long long)bits[q]);
         P.trace[3 * (it - 1) + q] = mx[q];
     }
     P.ctl[0] = it + 1;
@@ -277,7 +334,11 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
         set_error("Gauss-Hermite did not converge for K=%d", o->K);
         return GQMAP_ERR_INVALID_ARG;
     }
+    for (int c = 0; c < o->K; ++c)
+        for (int r = 0; r < o->K; ++r) P.WW[r + o->K * c] = P.W[c] * P.W[r];  // WIWJ (:5-6)
     const size_t MN = (size_t)M * N;
+    const int g1 = (int)((4 * (int64_t)(M - 1) * (N - 1) + 255) / 256), nblk = (int)((2 * (int64_t)MN + 255) / 256);
+    P.nblk = nblk;
     // mu = flow (:9); sigma = rand(M,N,2) + 2 (:10, library RNG stream 3,
     // drawn on the device) unless given; rou = 0 (:11)
     // One device arena per host thread and device, kept across calls: the
@@ -288,7 +349,7 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     GQ_CHECK(device < kArenaDev, GQMAP_ERR_INVALID_ARG, "device %d >= %d", device, kArenaDev);
     const size_t sizes[9] = {sizeof(double) * 2 * MN, sizeof(double) * 2 * MN, sizeof(double) * 2 * MN,
                              sizeof(double) * 4 * MN, sizeof(double) * 4 * MN, sizeof(double) * 20 * MN,
-                             sizeof(unsigned long long) * 3 * (size_t)o->its, sizeof(int) * 4,
+                             sizeof(unsigned long long) * 3 * (size_t)nblk, sizeof(int) * 4,
                              sizeof(double) * 3 * (size_t)o->its};
     Buf *bufs[9] = {&bflow, &bmu, &bsg, &brou, &bdn, &bde, &bmax, &bctl, &btr};
     size_t need = 0;
@@ -316,19 +377,28 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     GQ_HIP(hipMemset(brou.p, 0, sizeof(double) * 4 * MN));
     GQ_HIP(hipMemset(bdn.p, 0, sizeof(double) * 4 * MN));   // dnode = zeros (:14): last row/col stay 0
     GQ_HIP(hipMemset(bde.p, 0, sizeof(double) * 20 * MN));  // dedge = zeros (:15)
-    GQ_HIP(hipMemset(bmax.p, 0, sizeof(unsigned long long) * 3 * (size_t)o->its));
     const int ctl0[4] = {1, 0, 0, 0};
     GQ_HIP(hipMemcpy(bctl.p, ctl0, sizeof(ctl0), hipMemcpyHostToDevice));
     P.flow = (const double *)bflow.p; P.mu = (double *)bmu.p; P.sigma = (double *)bsg.p; P.rou = (double *)brou.p;
-    P.dnode = (double *)bdn.p; P.dedge = (double *)bde.p; P.maxbits = (unsigned long long *)bmax.p;
+    P.dnode = (double *)bdn.p; P.dedge = (double *)bde.p; P.blkmax = (unsigned long long *)bmax.p;
     P.ctl = (int *)bctl.p; P.trace = (double *)btr.p;
-    const int g1 = (int)(((int64_t)(M - 1) * (N - 1) + 255) / 256), g2 = (int)((2 * (int64_t)MN + 255) / 256);
-    auto grad = P.gama == 1.0 ? (P.var == 1.0 ? k_legacy_grad<true, true> : k_legacy_grad<true, false>)
-                              : (P.var == 1.0 ? k_legacy_grad<false, true> : k_legacy_grad<false, false>);
+    // the grad kernel's compile-time variants: K = 9 (the reference's) or any
+    // K; gama / var == 1; dta == inf (the defaults)
+    using Grad = void (*)(LgParams);
+    static constexpr Grad kGrad[2][2][2][2] = {
+        {{{k_legacy_grad<0, false, false, false>, k_legacy_grad<0, false, false, true>},
+          {k_legacy_grad<0, false, true, false>, k_legacy_grad<0, false, true, true>}},
+         {{k_legacy_grad<0, true, false, false>, k_legacy_grad<0, true, false, true>},
+          {k_legacy_grad<0, true, true, false>, k_legacy_grad<0, true, true, true>}}},
+        {{{k_legacy_grad<9, false, false, false>, k_legacy_grad<9, false, false, true>},
+          {k_legacy_grad<9, false, true, false>, k_legacy_grad<9, false, true, true>}},
+         {{k_legacy_grad<9, true, false, false>, k_legacy_grad<9, true, false, true>},
+          {k_legacy_grad<9, true, true, false>, k_legacy_grad<9, true, true, true>}}}};
+    const Grad grad = kGrad[P.K == 9][P.gama == 1.0][P.var == 1.0][P.dta == INFINITY];
     for (int it = 0; it < o->its; ++it) {
         grad<<<g1, 256>>>(P);
-        k_legacy_update<<<g2, 256>>>(P);
-        k_legacy_ctl<<<1, 1>>>(P);
+        k_legacy_update<<<nblk, 256>>>(P);
+        k_legacy_ctl<<<1, 1024>>>(P);
     }
     GQ_HIP(hipGetLastError());
     GQ_HIP(hipDeviceSynchronize());
