@@ -912,10 +912,11 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                                                                      P.gh_xmax, R(ENG == 2 ? CTF_MARGIN : 0.0)));
         if (inner) {
             const auto fv = frame_view(P.VV, P.M2);
-            Sums<R> S = fast ? node_sums<ENG, false>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v,
-                                                     m, n + P.n_off)
-                             : node_sums<ENG, true>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u, mu_v,
-                                                    m, n + P.n_off);
+            constexpr bool PF = QA >= GQ_NODE_PF_MIN_Q;
+            Sums<R> S = fast ? node_sums<ENG, false, PF>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u,
+                                                         mu_v, m, n + P.n_off)
+                             : node_sums<ENG, true, PF>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u,
+                                                        mu_v, m, n + P.n_off);
             if (QA > 1) S = lane_combine<QA>(S);
             nd = node_epi(S, c, P.lamd, P.guard != 0, T, a, sg_u, sg_v, pn, ENG == 2);
             if constexpr (RS) {  // to the edge lane of the same node

@@ -26,6 +26,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <type_traits>
+
 namespace gq {
 
 #ifndef GQ_M_PI
@@ -229,6 +231,38 @@ GQ_HD R bicubic_cell4(VP VV, uint32_t o, uint32_t M2, R so, R to)
     return bicubic_w4<R>(VV, o, M2, s0, s1, s2, s3, t0, t1, t2, t3);
 }
 
+// The same interpolation split in two, so a loop can issue the next sample's
+// loads before this sample's arithmetic (node_sums, PF): the 16 taps of a
+// cell in their storage type, then bicubic_w4's fma chain on them.
+template <typename E>
+struct Taps16 {
+    E v[16];  // column-major: v[4 c + r], c columns from the cell's first tap
+};
+template <typename VP>
+GQ_HD auto load_taps16(VP VV, uint32_t o, uint32_t M2)
+{
+    using E = typename std::remove_cv<typename std::remove_reference<decltype(*VV)>::type>::type;
+    constexpr uint32_t EB = (uint32_t)sizeof(E);
+    const uint32_t ob = o * EB, cb = M2 * EB;
+    Taps16<E> T;
+    for (int c = 0; c < 4; ++c) {
+        const auto col = byte_ptr(VV, ob + (uint32_t)c * cb);
+        for (int r = 0; r < 4; ++r) T.v[4 * c + r] = col[r];
+    }
+    return T;
+}
+template <typename R, typename E>
+GQ_HD R bicubic_taps4(const Taps16<E> &T, R so, R to)
+{
+    R t0, t1, t2, t3, s0, s1, s2, s3;
+    keys4(to, t0, t1, t2, t3);
+    keys4(so, s0, s1, s2, s3);
+    R v[4];
+    for (int c = 0; c < 4; ++c)
+        v[c] = fma(R(T.v[4 * c + 3]), t3, fma(R(T.v[4 * c + 2]), t2, fma(R(T.v[4 * c + 1]), t1, R(T.v[4 * c]) * t0)));
+    return fma(s3, v[3], fma(s2, v[2], fma(s1, v[1], s0 * v[0])));
+}
+
 GQ_HD uint32_t cell_elem(int iy, int ix, int M2) { return (uint32_t)(iy - 1) + GQ_UMUL24(M2, ix - 1); }
 
 // Where the bicubic reads the padded frame: cell (iy, ix) (1-based) starts at
@@ -307,14 +341,21 @@ GQ_HD void axis_cell_rel(int j, R x, int n, int &ix, R &fr)
 // 4 x interp2-cubic at 1-based column jj + x1, row ii + x2 on the padded VV.
 // CLAMP = false: the caller guarantees 1 <= jj + x1 < No and 1 <= ii + x2 < Mo
 // for this sample, where every clamp is the identity -- same result.
+// cell4_v: the cell's first tap and the fractions, sample4_v: the value.
+template <bool CLAMP = true, typename TV, typename R>
+GQ_HD uint32_t cell4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2, R &so, R &to)
+{
+    int ix, iy;
+    axis_cell<CLAMP>(jj, x1, No, ix, so);
+    axis_cell<CLAMP>(ii, x2, Mo, iy, to);
+    return V.cell(iy, ix);
+}
 template <bool CLAMP = true, typename TV, typename R>
 GQ_HD R sample4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2)
 {
-    int ix, iy;
     R so, to;
-    axis_cell<CLAMP>(jj, x1, No, ix, so);
-    axis_cell<CLAMP>(ii, x2, Mo, iy, to);
-    return bicubic_cell4<R>(V.p, V.cell(iy, ix), V.ld, so, to);
+    const uint32_t o = cell4_v<CLAMP>(V, Mo, No, ii, jj, x1, x2, so, to);
+    return bicubic_cell4<R>(V.p, o, V.ld, so, to);
 }
 template <bool CLAMP = true, typename VP, typename R>
 GQ_HD R sample4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
@@ -323,13 +364,19 @@ GQ_HD R sample4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
 }
 // fp64 at absolute 1-based positions X (column), Y (row).
 template <bool CLAMP = true, typename TV>
-GQ_HD double sample4_abs_v(const TV &V, int Mo, int No, double X, double Y)
+GQ_HD uint32_t cell4_abs_v(const TV &V, int Mo, int No, double X, double Y, double &so, double &to)
 {
     int ix, iy;
-    double so, to;
     axis_cell_abs<CLAMP>(X, No, ix, so);
     axis_cell_abs<CLAMP>(Y, Mo, iy, to);
-    return bicubic_cell4<double>(V.p, V.cell(iy, ix), V.ld, so, to);
+    return V.cell(iy, ix);
+}
+template <bool CLAMP = true, typename TV>
+GQ_HD double sample4_abs_v(const TV &V, int Mo, int No, double X, double Y)
+{
+    double so, to;
+    const uint32_t o = cell4_abs_v<CLAMP>(V, Mo, No, X, Y, so, to);
+    return bicubic_cell4<double>(V.p, o, V.ld, so, to);
 }
 template <bool CLAMP = true, typename VP>
 GQ_HD double sample4_abs(VP VV, int M2, int Mo, int No, double X, double Y)
@@ -363,7 +410,7 @@ GQ_HD R round_ge1(R y)
 // same for rows; node_unclamped with CTF_MARGIN), so round(y) lies in [1, MM)
 // and no clamp or cap acts -- the same values.
 template <bool CLAMP = true, typename TV, typename R>
-GQ_HD R sample_ctf4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2)
+GQ_HD uint32_t cell_ctf4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2, R &so, R &to)
 {
     const R y = (((R)ii + x2) - R(1)) * R(64) + R(1), x = (((R)jj + x1) - R(1)) * R(64) + R(1);
     if constexpr (CLAMP) {
@@ -373,13 +420,24 @@ GQ_HD R sample_ctf4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2)
         int ix = (int)Xq, iy = (int)Yq;  // Xq in [1, No]: truncation == floor
         ix = ix > No - 1 ? No - 1 : ix;
         iy = iy > Mo - 1 ? Mo - 1 : iy;
-        return bicubic_cell4<R>(V.p, V.cell(iy, ix), V.ld, Xq - (R)ix, Yq - (R)iy);
+        so = Xq - (R)ix;
+        to = Yq - (R)iy;
+        return V.cell(iy, ix);
     } else {
         const R ry = trunc(y + R(0.5)), rx = trunc(x + R(0.5));  // y, x >= 1: round_ge1
         const R Yq = (ry - R(1)) * R(0.015625) + R(1), Xq = (rx - R(1)) * R(0.015625) + R(1);
         const int ix = (int)Xq, iy = (int)Yq;
-        return bicubic_cell4<R>(V.p, V.cell(iy, ix), V.ld, GQ_FRACT(Xq), GQ_FRACT(Yq));
+        so = GQ_FRACT(Xq);
+        to = GQ_FRACT(Yq);
+        return V.cell(iy, ix);
     }
+}
+template <bool CLAMP = true, typename TV, typename R>
+GQ_HD R sample_ctf4_v(const TV &V, int Mo, int No, int ii, int jj, R x1, R x2)
+{
+    R so, to;
+    const uint32_t o = cell_ctf4_v<CLAMP>(V, Mo, No, ii, jj, x1, x2, so, to);
+    return bicubic_cell4<R>(V.p, o, V.ld, so, to);
 }
 template <bool CLAMP = true, typename VP, typename R>
 GQ_HD R sample_ctf4(VP VV, int M2, int Mo, int No, int ii, int jj, R x1, R x2)
@@ -717,11 +775,42 @@ GQ_HD NodeCoef<R> node_coef(R o1, R o2, R p)
 // is clamped (node_unclamped), so the clamps are skipped -- same results.
 // V: where the taps are read (TapView: the frame, or the single-pixel
 // engines' staged window).
-template <int ENG, bool CLAMP = true, typename R, typename TP, typename TV, typename IP>
+// PF: software-pipelined -- sample k + dk's cell is located and its 16 taps
+// loaded before sample k's arithmetic, so the gather latency overlaps it
+// (the small-grid kernels run 1-2 waves per SIMD, memory waits dominating);
+// the same operations on the same operands, so the same bits.
+template <int ENG, bool CLAMP = true, bool PF = false, typename R, typename TP, typename TV, typename IP>
 GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, const TV &V, IP I1, int Mo, int No,
                         R eps, const NodeCoef<R> &c, R u1, R u2, int m, int n)
 {
     Sums<R> S;
+    if constexpr (PF && ENG != 1) {
+        const R I = I1[m + (int64_t)Mo * n];
+        constexpr bool ABS = ENG == 0 && sizeof(R) == 8;
+        const R U1 = ABS ? u1 + R(n + 1) : u1, U2 = ABS ? u2 + R(m + 1) : u2;
+        // cell and fractions of sample k
+        auto locate = [&](int k, R &so, R &to) -> uint32_t {
+            const R x1 = fma(c.ax, tab[tab_at(T_XI, k)], fma(c.bx, tab[tab_at(T_XJ, k)], U1));
+            const R x2 = fma(c.ay, tab[tab_at(T_XI, k)], fma(c.by, tab[tab_at(T_XJ, k)], U2));
+            if constexpr (ABS) return cell4_abs_v<CLAMP>(V, Mo, No, (double)x1, (double)x2, so, to);
+            else if constexpr (ENG == 2) return cell_ctf4_v<CLAMP>(V, Mo, No, m + 1, n + 1, x1, x2, so, to);
+            else return cell4_v<CLAMP>(V, Mo, No, m + 1, n + 1, x1, x2, so, to);
+        };
+        if (k0 < K2) {
+            const int klast = k0 + (K2 - 1 - k0) / dk * dk;
+            R so, to;
+            auto T = load_taps16(V.p, locate(k0, so, to), V.ld);
+            for (int k = k0; k <= klast; k += dk) {
+                const auto Tk = T;
+                const R sok = so, tok = to;
+                const int kn = k + dk <= klast ? k + dk : klast;  // the last pass reloads its own cell
+                T = load_taps16(V.p, locate(kn, so, to), V.ld);
+                const R d = fma(bicubic_taps4<R>(Tk, sok, tok), R(-0.25), I);
+                S.add(tab, k, GQ_SQRT(fma(d, d, eps)));
+            }
+        }
+        return S;
+    }
     if (ENG != 1) {
         const R I = I1[m + (int64_t)Mo * n];
         if constexpr (ENG == 0 && sizeof(R) == 8) {

@@ -51,6 +51,11 @@
 #ifndef GQ_PREFETCH_MIN_Q
 #define GQ_PREFETCH_MIN_Q 2
 #endif
+// Node quadrature software-pipelined (node_sums PF) from this many lanes per
+// node up (the latency-bound small grids); 99 = never
+#ifndef GQ_NODE_PF_MIN_Q
+#define GQ_NODE_PF_MIN_Q 99
+#endif
 #ifndef GQ_UNROLL_MIN_Q
 #define GQ_UNROLL_MIN_Q 2
 #endif

@@ -1,8 +1,9 @@
 """Profiling driver for one small grid (no torch): C3's middle pyramid levels
-(Grove3 resized, ctf K=11, the library's default lanes per node) or one
+(Grove3 full size or resized, ctf K=11, the library's default lanes per node) or one
 rank's share of the 8-way strong-scaling layout (RubberWhale 388 x 75,
 mixture K=9, Q=4, as a plain fused context).  Runs `its` iterations as
-replayed graphs after a warm-up.  usage: level_prof.py l240|l120|strip8 [its] [fp64|fp32]"""
+replayed graphs after a warm-up.  usage: level_prof.py l480|l240|l120|strip8 [its] [fp64|fp32]"""
+import hashlib
 import os
 import sys
 
@@ -19,10 +20,10 @@ from gqmap_opticalflow_amd import Engine, ctf_options, imresize, strip_split  # 
 case = sys.argv[1] if len(sys.argv) > 1 else "l240"
 its = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 prec = sys.argv[3] if len(sys.argv) > 3 else "fp64"
-if case in ("l240", "l120"):
+if case in ("l480", "l240", "l120"):
     I1, I2, flo, unk, o = gt_options("Grove3", 1, 11)
-    s = 0.5 if case == "l240" else 0.25
-    a, b = (np.asfortranarray(imresize(x, s)) for x in (I1, I2))
+    s = {"l480": 1.0, "l240": 0.5, "l120": 0.25}[case]
+    a, b = (np.asfortranarray(imresize(x, s) if s != 1 else x) for x in (I1, I2))
     opts = ctf_options(its=500, minu=o["minu"], maxu=o["maxu"], minv=o["minv"], maxv=o["maxv"])
     eng = Engine(opts, a, b, "ctf", prec)
 else:
@@ -35,4 +36,6 @@ with eng:
     eng.run(100)
     eng.init_state(0)
     done, tot, ker = eng.run_timed(its)
-    print(f"{case} {a.shape[0]}x{a.shape[1]} {prec} Q={eng.info().split}: k_iter {ker / done * 1e3:.1f} us/it")
+    chk = hashlib.sha1(np.ascontiguousarray(eng.map()).tobytes()).hexdigest()[:12]  # same bits across variants
+    print(f"{case} {a.shape[0]}x{a.shape[1]} {prec} Q={eng.info().split}: k_iter {ker / done * 1e3:.1f} us/it "
+          f"chk={chk}")
