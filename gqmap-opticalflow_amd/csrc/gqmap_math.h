@@ -967,17 +967,39 @@ GQ_HD double lit_interp(VP VV, int M2, int Mo, int No, double Xq, double Yq)
     return Vq / 4;
 }
 
+// x / y correctly rounded, given yr = RN(1 / y) (GQ_LIT_MDIV, device only):
+// q0 = RN(x yr) is within 1.5 ulp of x / y, one correction
+// RN(q0 + RN(x - y q0) yr) brings it within 1 ulp, and a second is RN(x / y)
+// exactly (Markstein's theorem: yr within half an ulp of 1 / y, q within one
+// ulp of x / y; no overflow or underflow for these operands) -- 5 operations
+// instead of the 12 of the general IEEE sequence; the host divides.
+#ifndef GQ_LIT_MDIV
+#define GQ_LIT_MDIV 0
+#endif
+GQ_HD double div_rcp(double x, double y, double yr)
+{
+#if GQ_LIT_MDIV && defined(__HIP_DEVICE_COMPILE__)
+    double q = x * yr;
+    q = fma(fma(-q, y, x), yr, q);
+    return fma(fma(-q, y, x), yr, q);
+#else
+    (void)yr;
+    return x / y;
+#endif
+}
+
 // The six accumulators of the quadrature loop (gqmap_gpu_mixture.m:98-105)
 struct LitAcc {
     double dp = 0, du1 = 0, du2 = 0, do1 = 0, do2 = 0, Ei = 0;
     template <typename TP>
-    GQ_HD void add(TP tab, int k, double fval, double zi, double zj, double p, double sqrtpr, bool live)
+    GQ_HD void add(TP tab, int k, double fval, double zi, double zj, double p, double sqrtpr, double rsqrtpr,
+                   bool live)
     {
         if (live) {  // `if a~=0` (:98)
             dp = dp + fval * ((p - p * tab[tab_at(TL_A, k)]) + tab[tab_at(TL_X2, k)]);
             du1 = du1 + fval * (zi - p * zj);
             du2 = du2 + fval * (zj - p * zi);
-            const double q = tab[tab_at(TL_M, k)] / sqrtpr;
+            const double q = div_rcp(tab[tab_at(TL_M, k)], sqrtpr, rsqrtpr);
             do1 = do1 + fval * (tab[tab_at(TL_A1, k)] + q);
             do2 = do2 + fval * (tab[tab_at(TL_A1, k)] - q);
         }
@@ -987,7 +1009,7 @@ struct LitAcc {
 
 // Spectral coordinates shared by both gradients (:90-93, :120-123)
 struct LitCoef {
-    double s, t, pr, sqrtpr;
+    double s, t, pr, sqrtpr, rsqrtpr;  // rsqrtpr = RN(1 / sqrtpr) (div_rcp)
 };
 GQ_HD LitCoef lit_coef(double p)
 {
@@ -997,6 +1019,7 @@ GQ_HD LitCoef lit_coef(double p)
     c.t = (sp - sm) / 2;
     c.pr = 1 - p * p;
     c.sqrtpr = GQ_SQRT(c.pr);
+    c.rsqrtpr = 1 / c.sqrtpr;
     return c;
 }
 
@@ -1043,7 +1066,7 @@ GQ_HD Grad<double> lit_node_grad(TP tab, int K2, VP VV, int M2, IP I1, int Mo, i
         const double x1 = so1 * zi + u1, x2 = so2 * zj + u2;
         const double d = I - lit_interp(VV, M2, Mo, No, (double)(n + 1) + x1, (double)(m + 1) + x2);
         const double fval = tab[tab_at(TL_W, k)] * (-lamd * GQ_SQRT(eps + d * d));
-        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, live);
+        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, c.rsqrtpr, live);
     }
     return lit_epi(S, c, a, o1, o2, p, T, true);
 }
@@ -1062,7 +1085,7 @@ GQ_HD Grad<double> lit_edge_grad(TP tab, int K2, double eps, double lams, bool g
         const double zi = c.s * XI + c.t * XJ, zj = c.t * XI + c.s * XJ;
         const double d = (so1 * zi + u1) - (so2 * zj + u2);
         const double fval = tab[tab_at(TL_W, k)] * (-lams * GQ_SQRT(eps + d * d));
-        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, live);
+        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, c.rsqrtpr, live);
     }
     return lit_epi(S, c, a, o1, o2, p, T, false);
 }

@@ -22,6 +22,8 @@ else:
     I1, I2, flo, unk, o = setup_problem("rubberwhale", 1, 9)
 if os.environ.get("GQMAP_SPLIT"):
     o["split"] = int(os.environ["GQMAP_SPLIT"])
+if os.environ.get("GQMAP_ARITH"):  # "literal": the literal-order engine
+    o["arith"] = os.environ["GQMAP_ARITH"]
 with Engine(o, I1, I2, engine, prec) as eng:
     eng.init_state(0)
     done, tot, ker = eng.run_timed(its)
