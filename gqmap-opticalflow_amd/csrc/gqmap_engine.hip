@@ -912,7 +912,9 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                                                                      P.gh_xmax, R(ENG == 2 ? CTF_MARGIN : 0.0)));
         if (inner) {
             const auto fv = frame_view(P.VV, P.M2);
-            constexpr bool PF = QA >= GQ_NODE_PF_MIN_Q;
+            // (at one lane per node only with float taps: the fp64-tap Q = 1
+            // kernels would cross 168 VGPRs, 3 -> 2 waves per SIMD)
+            constexpr bool PF = QA >= GQ_NODE_PF_MIN_Q && (QA > 1 || sizeof(VT) == 4);
             Sums<R> S = fast ? node_sums<ENG, false, PF>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u,
                                                          mu_v, m, n + P.n_off)
                              : node_sums<ENG, true, PF>(tab, kj, K2, QA, fv, P.I1, P.Mo, P.No, P.epsn, c, mu_u,

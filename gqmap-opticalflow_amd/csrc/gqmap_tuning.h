@@ -52,9 +52,11 @@
 #define GQ_PREFETCH_MIN_Q 2
 #endif
 // Node quadrature software-pipelined (node_sums PF) from this many lanes per
-// node up (the latency-bound small grids); 99 = never
+// node up; 99 = never.  Round 5 (profiles/r05_node_pf_ab.txt): C2 fp64
+// k_iter -1.3%, ctf 480x640 -0.5%, 388x75 strip -1%, 240x320 / 120x160
+// unchanged, same bits; the C2 kernel at 164 VGPRs instead of 168.
 #ifndef GQ_NODE_PF_MIN_Q
-#define GQ_NODE_PF_MIN_Q 99
+#define GQ_NODE_PF_MIN_Q 1
 #endif
 #ifndef GQ_UNROLL_MIN_Q
 #define GQ_UNROLL_MIN_Q 2
