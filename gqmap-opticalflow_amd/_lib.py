@@ -34,7 +34,7 @@ EXPORTS = (
     "gqmap_ctf_get_level", "gqmap_ctf_set_truth", "gqmap_ctf_get_trace", "gqmap_ctf_destroy", "gqmap_resize_len", "gqmap_create_tile",
     "gqmap_comm_unique_id", "gqmap_tile_attach_rccl", "gqmap_tile_group_run", "gqmap_tile_attach_host",
     "gqmap_tile_exchange_sizes", "gqmap_tile_exchange_begin", "gqmap_tile_exchange_end",
-    "gqmap_cpu_options_default", "gqmap_cpu_run", "gqmap_cpu_release", "gqmap_read_flo", "gqmap_write_flo", "gqmap_aepe",
+    "gqmap_cpu_options_default", "gqmap_cpu_run", "gqmap_cpu_run_device", "gqmap_cpu_release", "gqmap_read_flo", "gqmap_write_flo", "gqmap_aepe",
 )
 CTF_MAX_LEVELS = 8
 
@@ -150,6 +150,8 @@ def load():
         "gqmap_aepe": (C.c_int, [_D, _D, u8, C.c_int, C.c_int, C.c_int, _D]),
         "gqmap_cpu_run": (C.c_int, [P(GqmapCpuOptions), _D, C.c_int, C.c_int, _D, C.c_uint64, _D, _D, _D, _D,
                                     P(C.c_int), C.c_int]),
+        "gqmap_cpu_run_device": (C.c_int, [P(GqmapCpuOptions), vp, C.c_int, C.c_int, vp, C.c_uint64, vp, vp, vp,
+                                           vp, P(C.c_int), C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -310,13 +310,30 @@ gqmap_status gqmap_cpu_release(void)
     return GQMAP_OK;
 }
 
-gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int N, const double *sigma0,
-                           uint64_t seed, double *mu, double *sigma, double *rou, double *trace, int *its_done,
-                           int device)
+}  // extern "C"
+
+namespace {
+
+// Does p point into device memory of the current device (or managed memory)?
+bool on_device(const void *p)
 {
-    clear_error();
-    GQ_CHECK(o && flow && mu && sigma && rou, GQMAP_ERR_INVALID_ARG, "gqmap_cpu_run: null argument");
-    GQ_CHECK(M >= 2 && N >= 2, GQMAP_ERR_INVALID_ARG, "gqmap_cpu_run: flow %dx%d too small", M, N);
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // a plain host pointer: clear the sticky error
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+// gqmap_cpu_run (DEV = false: host arrays, copied in and out) and
+// gqmap_cpu_run_device (DEV = true: flow / sigma0 / mu / sigma / rou / trace
+// are device arrays; the iteration runs on mu / sigma / rou in place).
+gqmap_status cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int N, const double *sigma0, uint64_t seed,
+                     double *mu, double *sigma, double *rou, double *trace, int *its_done, int device, bool DEV)
+{
+    const char *fn = DEV ? "gqmap_cpu_run_device" : "gqmap_cpu_run";
+    GQ_CHECK(o && flow && mu && sigma && rou, GQMAP_ERR_INVALID_ARG, "%s: null argument", fn);
+    GQ_CHECK(M >= 2 && N >= 2, GQMAP_ERR_INVALID_ARG, "%s: flow %dx%d too small", fn, M, N);
     GQ_CHECK(o->K >= 1 && o->K <= GQMAP_KMAX, GQMAP_ERR_INVALID_ARG, "K=%d outside [1,%d]", o->K, GQMAP_KMAX);
     GQ_CHECK(o->its >= 1, GQMAP_ERR_INVALID_ARG, "its=%d", o->its);
     int ndev = 0;
@@ -325,7 +342,16 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
         return GQMAP_ERR_NO_DEVICE;
     }
     GQ_CHECK(device >= 0 && device < ndev, GQMAP_ERR_INVALID_ARG, "device %d of %d", device, ndev);
+    GQ_CHECK(device < kArenaDev, GQMAP_ERR_INVALID_ARG, "device %d >= %d", device, kArenaDev);
     DeviceGuard dg(device);
+    const size_t MN = (size_t)M * N;
+    if (DEV) {
+        GQ_CHECK(on_device(flow) && on_device(mu) && on_device(sigma) && on_device(rou) &&
+                     (!sigma0 || on_device(sigma0)) && (!trace || on_device(trace)),
+                 GQMAP_ERR_INVALID_ARG, "%s: every array must be device memory", fn);
+        GQ_CHECK(mu != flow && (const double *)sigma != sigma0, GQMAP_ERR_INVALID_ARG,
+                 "%s: mu must not alias flow, nor sigma sigma0", fn);
+    }
     LgParams P{};
     P.M = M; P.N = N; P.K = o->K; P.its = o->its; P.min_its = o->min_its;
     P.var = o->var; P.gama = o->gama; P.dta = o->dta; P.step0 = o->step0; P.step_decay = o->step_decay;
@@ -336,21 +362,19 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     }
     for (int c = 0; c < o->K; ++c)
         for (int r = 0; r < o->K; ++r) P.WW[r + o->K * c] = P.W[c] * P.W[r];  // WIWJ (:5-6)
-    const size_t MN = (size_t)M * N;
     const int g1 = (int)((4 * (int64_t)(M - 1) * (N - 1) + 255) / 256), nblk = (int)((2 * (int64_t)MN + 255) / 256);
     P.nblk = nblk;
-    // mu = flow (:9); sigma = rand(M,N,2) + 2 (:10, library RNG stream 3,
-    // drawn on the device) unless given; rou = 0 (:11)
     // One device arena per host thread and device, kept across calls: the
-    // nine buffers (~300 B per pixel) are carved from it, so a repeated call
-    // pays no hipMalloc/hipFree (they dominated a 50-iteration call's wall clock).
+    // buffers (~300 B per pixel with host arrays, ~200 with device arrays)
+    // are carved from it, so a repeated call pays no hipMalloc/hipFree (they
+    // dominated a 50-iteration call's wall clock).
     struct Buf { void *p = nullptr; };
     Buf bflow, bmu, bsg, brou, bdn, bde, bmax, bctl, btr;
-    GQ_CHECK(device < kArenaDev, GQMAP_ERR_INVALID_ARG, "device %d >= %d", device, kArenaDev);
-    const size_t sizes[9] = {sizeof(double) * 2 * MN, sizeof(double) * 2 * MN, sizeof(double) * 2 * MN,
-                             sizeof(double) * 4 * MN, sizeof(double) * 4 * MN, sizeof(double) * 20 * MN,
+    const size_t io = DEV ? 0 : 1, tr = DEV && trace ? 0 : 1;
+    const size_t sizes[9] = {io * sizeof(double) * 2 * MN, io * sizeof(double) * 2 * MN, io * sizeof(double) * 2 * MN,
+                             io * sizeof(double) * 4 * MN, sizeof(double) * 4 * MN, sizeof(double) * 20 * MN,
                              sizeof(unsigned long long) * 3 * (size_t)nblk, sizeof(int) * 4,
-                             sizeof(double) * 3 * (size_t)o->its};
+                             tr * sizeof(double) * 3 * (size_t)o->its};
     Buf *bufs[9] = {&bflow, &bmu, &bsg, &brou, &bdn, &bde, &bmax, &bctl, &btr};
     size_t need = 0;
     for (size_t sz : sizes) need += (sz + 255) & ~(size_t)255;
@@ -368,10 +392,20 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
         bufs[i]->p = (char *)A.p + off;
         off += (sizes[i] + 255) & ~(size_t)255;
     }
-    GQ_HIP(hipMemcpy(bflow.p, flow, sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
+    if (DEV) {
+        bflow.p = const_cast<double *>(flow);
+        bmu.p = mu;
+        bsg.p = sigma;
+        brou.p = rou;
+        if (trace) btr.p = trace;
+    } else {
+        GQ_HIP(hipMemcpy(bflow.p, flow, sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
+    }
+    // mu = flow (:9); sigma = rand(M,N,2) + 2 (:10, library RNG stream 3,
+    // drawn on the device) unless given; rou = 0 (:11)
     GQ_HIP(hipMemcpy(bmu.p, bflow.p, sizeof(double) * 2 * MN, hipMemcpyDeviceToDevice));
     if (sigma0)
-        GQ_HIP(hipMemcpy(bsg.p, sigma0, sizeof(double) * 2 * MN, hipMemcpyHostToDevice));
+        GQ_HIP(hipMemcpy(bsg.p, sigma0, sizeof(double) * 2 * MN, DEV ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
     else
         k_legacy_sigma0<<<(int)((2 * MN + 255) / 256), 256>>>((double *)bsg.p, (int64_t)(2 * MN), stream_base(seed, 3));
     GQ_HIP(hipMemset(brou.p, 0, sizeof(double) * 4 * MN));
@@ -404,12 +438,35 @@ gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M
     GQ_HIP(hipDeviceSynchronize());
     int ctl[4];
     GQ_HIP(hipMemcpy(ctl, bctl.p, sizeof(ctl), hipMemcpyDeviceToHost));
-    GQ_HIP(hipMemcpy(mu, bmu.p, sizeof(double) * 2 * MN, hipMemcpyDeviceToHost));
-    GQ_HIP(hipMemcpy(sigma, bsg.p, sizeof(double) * 2 * MN, hipMemcpyDeviceToHost));
-    GQ_HIP(hipMemcpy(rou, brou.p, sizeof(double) * 4 * MN, hipMemcpyDeviceToHost));
-    if (trace) GQ_HIP(hipMemcpy(trace, btr.p, sizeof(double) * 3 * (size_t)ctl[2], hipMemcpyDeviceToHost));
+    if (!DEV) {
+        GQ_HIP(hipMemcpy(mu, bmu.p, sizeof(double) * 2 * MN, hipMemcpyDeviceToHost));
+        GQ_HIP(hipMemcpy(sigma, bsg.p, sizeof(double) * 2 * MN, hipMemcpyDeviceToHost));
+        GQ_HIP(hipMemcpy(rou, brou.p, sizeof(double) * 4 * MN, hipMemcpyDeviceToHost));
+        if (trace)
+            GQ_HIP(hipMemcpy(trace, btr.p, sizeof(double) * 3 * (size_t)ctl[2], hipMemcpyDeviceToHost));
+    }
     if (its_done) *its_done = ctl[2];
     return GQMAP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int N, const double *sigma0,
+                           uint64_t seed, double *mu, double *sigma, double *rou, double *trace, int *its_done,
+                           int device)
+{
+    clear_error();
+    return cpu_run(o, flow, M, N, sigma0, seed, mu, sigma, rou, trace, its_done, device, false);
+}
+
+gqmap_status gqmap_cpu_run_device(const gqmap_cpu_options *o, const double *flow, int M, int N,
+                                  const double *sigma0, uint64_t seed, double *mu, double *sigma, double *rou,
+                                  double *trace, int *its_done, int device)
+{
+    clear_error();
+    return cpu_run(o, flow, M, N, sigma0, seed, mu, sigma, rou, trace, its_done, device, true);
 }
 
 }  // extern "C"

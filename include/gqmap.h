@@ -303,6 +303,16 @@ void gqmap_cpu_options_default(gqmap_cpu_options *o);
 gqmap_status gqmap_cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int N,
                            const double *sigma0, uint64_t seed, double *mu, double *sigma, double *rou,
                            double *trace, int *its_done, int device);
+/* gqmap_cpu_run with device arrays (inputs already resident in HBM, no host
+ * copies): flow, sigma0 (or NULL), mu, sigma, rou and trace (or NULL) point
+ * to memory of `device`, in the layouts above; the iteration runs on mu /
+ * sigma / rou in place; *its_done is a host int.  Same results as
+ * gqmap_cpu_run bit for bit.  GQMAP_ERR_INVALID_ARG for a host array or mu
+ * aliasing flow.  (Reference counterpart: the same gqmap_cpu.m call on
+ * gpuArray inputs.) */
+gqmap_status gqmap_cpu_run_device(const gqmap_cpu_options *o, const double *flow, int M, int N,
+                                  const double *sigma0, uint64_t seed, double *mu, double *sigma, double *rou,
+                                  double *trace, int *its_done, int device);
 /* gqmap_cpu_run keeps its device buffers in a per-thread, per-device arena
  * across calls (a call needing under a quarter of it shrinks it); this frees
  * the calling thread's arenas now.  Replaces nothing in the reference (the

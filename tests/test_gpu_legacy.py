@@ -65,3 +65,45 @@ def test_legacy_ragged_sizes_bit_exact(shape):
     legacy.release()
     with pytest.raises(ValueError):
         gqmap_cpu(o, flow, sigma0=sg0[:, :, 0])
+
+
+def test_legacy_device_arrays_same_bits_as_host_arrays():
+    """gqmap_cpu_run_device (flow resident in HBM, outputs left there) gives
+    the host-array call's results bit for bit, with a given sigma0 and with the
+    library RNG, and stops at the same iteration (the stop rule, :70)."""
+    import torch
+    from gqmap_opticalflow_amd import gqmap_cpu, gqmap_cpu_device
+    rng = np.random.default_rng(11)
+    M, N = 45, 52
+    flow = np.asfortranarray(rng.normal(0, 2, (M, N, 2)))
+    sg0 = np.asfortranarray(rng.uniform(0, 1, (M, N, 2)) + 2)
+    dev = torch.device("cuda", 0)
+    flow_d = torch.from_numpy(flow).to(dev)
+    sg0_d = torch.from_numpy(sg0).to(dev)
+    assert flow_d.stride() == (1, M, M * N)
+    for kw_h, kw_d, its in (({"sigma0": sg0}, {"sigma0": sg0_d}, 40), ({"seed": 3}, {"seed": 3}, 150)):
+        o = dict(its=its, K=9, min_its=100, tor=1e-1)
+        h = gqmap_cpu(o, flow, return_trace=True, **kw_h)
+        d = gqmap_cpu_device(o, flow_d, return_trace=True, **kw_d)
+        for a, b, k in zip(h, d, ("mu", "sigma", "rou", "trace")):
+            np.testing.assert_array_equal(a, b.cpu().numpy(), err_msg=k)
+    # the input flow is left as it was
+    np.testing.assert_array_equal(flow_d.cpu().numpy(), flow)
+
+
+def test_legacy_device_arrays_rejects_host_and_row_major():
+    import torch
+    from gqmap_opticalflow_amd import gqmap_cpu_device, legacy
+    from gqmap_opticalflow_amd._lib import load
+    import ctypes as C
+    flow = np.zeros((8, 9, 2), order="F")
+    with pytest.raises(ValueError):  # row-major device tensor
+        gqmap_cpu_device({}, torch.zeros((8, 9, 2), dtype=torch.float64, device="cuda"))
+    with pytest.raises(TypeError):
+        gqmap_cpu_device({}, torch.from_numpy(flow))  # host tensor
+    # the C-ABI itself refuses host pointers
+    o = legacy.cpu_options({"its": 2})
+    out = [np.zeros((8, 9, 2), order="F"), np.zeros((8, 9, 2), order="F"), np.zeros((8, 9, 2, 2), order="F")]
+    rc = load().gqmap_cpu_run_device(C.byref(o), flow.ctypes.data, 8, 9, None, C.c_uint64(0),
+                                     *[a.ctypes.data for a in out], None, None, 0)
+    assert rc != 0
