@@ -971,7 +971,8 @@ GQ_HD double lit_interp(VP VV, int M2, int Mo, int No, double Xq, double Yq)
 // q0 = RN(x yr) is within 1.5 ulp of x / y, one correction
 // RN(q0 + RN(x - y q0) yr) brings it within 1 ulp, and a second is RN(x / y)
 // exactly (Markstein's theorem: yr within half an ulp of 1 / y, q within one
-// ulp of x / y; no overflow or underflow for these operands) -- 5 operations
+// ulp of x / y; no overflow or underflow for these operands: |x| < 64 and
+// sqrtpr >= sqrt(1 - corr_tor^2) > 0, |p| <= corr_tor < 1) -- 5 operations
 // instead of the 12 of the general IEEE sequence; the host divides.  Round 5
 // (profiles/r05_literal_div_ab.txt): the literal engine's k_iter 327 -> 298 us
 // on C2, still bit-identical to the restatement over 500 iterations.
