@@ -30,7 +30,8 @@ named in `config`):
     --config c2 --tiled   the RubberWhale pair itself split over the ranks
                   (strong scaling of the headline pair)
     --config c1   Dimetrodon 388x584 legacy/gqmap_cpu.m flow denoising, 50 its
-                  (device drop-in; timed call includes its host<->device copies)
+                  (gqmap_cpu_run_device on the flow resident in HBM; the
+                  host-array call's PCIe-inclusive rate as `host_arrays`)
 Before the timed steps (after --warmup W steps and the graph capture) the
 hot path runs untimed until the GPU clocks settle (settle_clocks; reported as
 `clock_settle`, with the same steps timed once cold as `cold_start_value`;
