@@ -1921,11 +1921,19 @@ namespace {
 // (choose_lpar) and counts node-components: C4 (120x160 x L=3 = 57,600)
 // Q = 16 / 4 / 1 -> 616 / 509 / 613-717 us with global table reads (one block
 // per tile: 680 / 829 / 1687); Q = 4 with the LDS table 376 us.
-int choose_split(int M, int N, int L, int forced, bool super_)
+// Lanes per node from the node count.  Single-scale mixture (round 5,
+// profiles/r05_strip_q_sweep.txt, RubberWhale strips 388 x 21..294): Q = 1
+// from 98,304 nodes (114k: 87 vs 101 us at Q = 2), Q = 2 from 16,384 (76k:
+// 80 vs 86 at Q = 1; 57k: 57 vs 69 at Q = 4; 20k: 38.7 vs 39.5), Q = 4
+// below (15k: 30 vs 38).  Coarse-to-fine levels (K = 11; round 2-3 sweeps,
+// profiles/r03_midq_sweep.txt): Q = 1 from 2^17, 2 from 2^16, 4 from 2^13.
+int choose_split(int M, int N, int L, int forced, bool super_, bool ctf)
 {
     if (forced == 1 || forced == 2 || forced == 4 || forced == 8 || forced == 16 || (forced == 64 && !super_))
         return forced;
     const int64_t nodes = (int64_t)M * N;
+    if (!super_ && !ctf)
+        return nodes >= 98304 ? 1 : nodes >= (1 << 14) ? 2 : nodes >= (1 << 13) ? 4 : nodes >= (1 << 11) ? 8 : 64;
     if (!super_)
         return nodes >= (1 << 17) ? 1 : nodes >= (1 << 16) ? 2 : nodes >= (1 << 13) ? 4 : nodes >= (1 << 11) ? 8 : 64;
     const int64_t nl = nodes * L;
@@ -1979,7 +1987,9 @@ void tile_grid(gqmap_ctx *c)
 {
     // from the whole grid (Ng columns), so every column-strip tile sums its
     // quadrature in the same order as the untiled solve
-    c->split = c->lit ? 1 : choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_);
+    c->split = c->lit ? 1
+                      : choose_split(c->M, c->Ng > 0 ? c->Ng : c->N, c->super_ ? c->L : 1, c->opt.split, c->super_,
+                                     c->opt.engine == GQMAP_ENGINE_CTF);
     c->kq = c->split;
     if (c->opt.split == GQMAP_SPLIT_ROLE && !c->super_) {  // role split: Q = 1 arithmetic
         c->split = 1;

@@ -278,17 +278,17 @@ class Engine:
 
 
 def strip_split(M: int, N: int, n_tiles: int) -> int:
-    """Lanes per node Q for a single-pixel engine grid M x N cut into n_tiles
+    """Lanes per node Q for a single-scale mixture grid M x N cut into n_tiles
     column strips, chosen from ONE strip's node count with the library's own
-    thresholds (gqmap_engine.hip choose_split: Q = 1 from 2^17 nodes, 2 from
-    2^16, 4 from 2^13, 8 from 2^11, else 64 -- one wave per node).  The
-    library picks Q from the whole grid so a tiled solve sums in the untiled
-    order; pass this as options["split"] to every tile AND to the whole-grid
-    reference to keep both bit-identical while each rank's strip still fills
-    the GPU (strong scaling).  tests/test_tiles.py pins these thresholds
-    against the library's."""
+    thresholds (gqmap_engine.hip choose_split, mixture: Q = 1 from 98,304
+    nodes, 2 from 2^14, 4 from 2^13, 8 from 2^11, else 64 -- one wave per
+    node).  The library picks Q from the whole grid so a tiled solve sums in
+    the untiled order; pass this as options["split"] to every tile AND to the
+    whole-grid reference to keep both bit-identical while each rank's strip
+    still fills the GPU (strong scaling).  tests/test_tiles.py pins these
+    thresholds against the library's."""
     nodes = M * -(-N // max(1, n_tiles))
-    return (1 if nodes >= 1 << 17 else 2 if nodes >= 1 << 16 else 4 if nodes >= 1 << 13
+    return (1 if nodes >= 98304 else 2 if nodes >= 1 << 14 else 4 if nodes >= 1 << 13
             else 8 if nodes >= 1 << 11 else 64)
 
 

@@ -259,10 +259,14 @@ def get_map(alpha, muu, sigu, muv, sigv, nthreads: int = 0, det_exp: bool = Fals
     return out
 
 
-def split_for(M: int, N: int, super_: bool = False, L: int = 1) -> int:
-    """The library's default lanes-per-node policy (gqmap_engine.hip choose_split;
+def split_for(M: int, N: int, super_: bool = False, L: int = 1, ctf: bool = False) -> int:
+    """The library's default lanes-per-node policy (gqmap_engine.hip choose_split:
+    single-scale mixture and coarse-to-fine levels have their own thresholds;
     the super engine runs its L components as separate blocks: nodes x L)."""
     nodes = M * N
+    if not super_ and not ctf:
+        return (1 if nodes >= 98304 else 2 if nodes >= (1 << 14) else 4 if nodes >= (1 << 13)
+                else 8 if nodes >= (1 << 11) else 64)
     if not super_:
         return (1 if nodes >= (1 << 17) else 2 if nodes >= (1 << 16) else 4 if nodes >= (1 << 13)
                 else 8 if nodes >= (1 << 11) else 64)
@@ -287,7 +291,8 @@ def emu_run(opts: dict, I1, I2, state: State, it_first: int, n_iter: int, X, W,
     f.restype = C.c_int
     Q = int(opts.get("split", 0))
     Q = 1 if Q == -1 else Q  # GQMAP_SPLIT_ROLE: a kernel shape with the Q = 1 arithmetic
-    Q = Q or (split_for(p.M, p.N, bool(p.super_), int(p.L)) if split is None else split)
+    Q = Q or (split_for(p.M, p.N, bool(p.super_), int(p.L), opts.get("engine") == "ctf")
+              if split is None else split)
     done = f(C.byref(p), _p(X), _p(W), _p(I1), _p(VV), C.byref(cs), Tbox, it_first, n_iter,
              _p(trace), nthreads, int(fp32), Q)
     if done < 0:

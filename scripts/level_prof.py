@@ -2,7 +2,8 @@
 (Grove3 full size or resized, ctf K=11, the library's default lanes per node) or one
 rank's share of the 8-way strong-scaling layout (RubberWhale 388 x 75,
 mixture K=9, Q=4, as a plain fused context).  Runs `its` iterations as
-replayed graphs after a warm-up.  usage: level_prof.py l480|l240|l120|strip8 [its] [fp64|fp32]"""
+replayed graphs after a warm-up.  usage: level_prof.py l480|l240|l120|strip2|strip4|strip8 [its] [fp64|fp32]
+(GQMAP_SPLIT=q forces the strips' lanes per node)"""
 import hashlib
 import os
 import sys
@@ -26,11 +27,13 @@ if case in ("l480", "l240", "l120"):
     a, b = (np.asfortranarray(imresize(x, s) if s != 1 else x) for x in (I1, I2))
     opts = ctf_options(its=500, minu=o["minu"], maxu=o["maxu"], minv=o["minv"], maxv=o["maxv"])
     eng = Engine(opts, a, b, "ctf", prec)
-else:
+else:  # stripN: one rank's column strip of the N-way layout (+2 ghost columns)
+    nt = int(case[5:] or 8)
     I1, I2, flo, unk, o = gt_options("rubberwhale", 1, 9)
-    w = -(-I1.shape[1] // 8) + 2
+    w = -(-I1.shape[1] // nt) + 2
     a, b = (np.asfortranarray(x[:, :w]) for x in (I1, I2))
-    eng = Engine(dict(o, split=strip_split(I1.shape[0], I1.shape[1], 8)), a, b, "mixture", prec)
+    q = int(os.environ.get("GQMAP_SPLIT") or strip_split(I1.shape[0], I1.shape[1], nt))
+    eng = Engine(dict(o, split=q), a, b, "mixture", prec)
 with eng:
     eng.init_state(0)
     eng.run(100)

@@ -210,18 +210,18 @@ def test_host_staged_tiles_three_processes_bit_exact(tmp_path):
     assert cols[0][0] == 0 and cols[-1][1] == ref.muu.shape[1]
 
 
-@pytest.mark.parametrize("n_tiles", [2, 8])
+@pytest.mark.parametrize("n_tiles", [2, 4, 8])
 def test_c2_pair_strips_at_per_strip_split_bit_exact(n_tiles):
     """The strong-scaling layout of the headline pair (bench.py strong_scaling):
     the full RubberWhale frame (388x584) as n_tiles column strips whose lanes
-    per node come from ONE strip (strip_split: Q = 2 for 2 strips, 4 for 8),
+    per node come from ONE strip (strip_split: Q = 1 for 2 strips, 2 for 4 and 8),
     on one GPU through the in-process transport -- bit-identical to the
     whole-grid solve run at the same Q."""
     from gqmap_opticalflow_amd import Engine, flow_to_color, flowio, strip_split, tile_group_run
     I1, I2, gt = flowio.load_pair("rubberwhale")
     _, _, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
     q = strip_split(*I1.shape, n_tiles)
-    assert q == {2: 2, 8: 4}[n_tiles]
+    assert q == {2: 1, 4: 2, 8: 2}[n_tiles]
     o = dict(K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdad=1.0, lambdas=5.0,
              minu=minu, maxu=maxu, minv=minv, maxv=maxv, split=q)
     its = 30

@@ -201,7 +201,13 @@ def test_strip_split_mirrors_library_thresholds():
     for M in (30, 60, 120, 240, 388, 480):
         for N in (40, 80, 160, 320, 584, 640):
             assert strip_split(M, N, 1) == oracle.split_for(M, N), (M, N)
-    assert strip_split(388, 584, 8) == 4 and strip_split(388, 584, 2) == 2 and strip_split(30, 40, 2) == 64
+    # the headline pair's strips (round 5 mixture thresholds): 2-way Q=1, 4- and 8-way Q=2, 16-way Q=4
+    assert [strip_split(388, 584, n) for n in (1, 2, 4, 8, 16)] == [1, 1, 2, 2, 4]
+    assert strip_split(30, 40, 2) == 64
+    # the coarse-to-fine levels keep their own thresholds
+    assert oracle.split_for(240, 320, ctf=True) == 2 and oracle.split_for(240, 320) == 2
+    assert oracle.split_for(120, 160, ctf=True) == 4 and oracle.split_for(120, 160) == 2
+    assert oracle.split_for(388, 300, ctf=True) == 2 and oracle.split_for(388, 300) == 1
 
 
 @pytest.mark.parametrize("engine", ["mixture", "super"])
