@@ -29,6 +29,10 @@ LIMITS = {
     "_ZN2gq6k_iterIddLi0ELi1ELb1EEEvNS_10IterParamsIT_T0_EE": 168,
     "_ZN2gq6k_iterIddLi2ELi2ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
     "_ZN2gq6k_iterIdfLi1ELi4ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
+    # C3's 120x160 level (Q=4; 257 registers = 1 wave: 47.6 -> 72.5 us,
+    # profiles/r05_node_pair_ab.txt) and the strong-scaling strips (mixture Q=2)
+    "_ZN2gq6k_iterIddLi2ELi4ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
+    "_ZN2gq6k_iterIdfLi0ELi2ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
 }
 
 
