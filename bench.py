@@ -503,7 +503,7 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     lit = None
     if engine == "mixture" and args.precision == "fp64" and not args.no_literal:
         try:
-            lit = literal_engine_leg(args, rank, barrier, opts, I1, I2, flo, unk, gate_its, local)
+            lit = literal_engine_leg(args, rank, opts, I1, I2, flo, unk, gate_its, local)
         except Exception as e:  # reported in the line; the headline value stands
             lit = {"error": f"{type(e).__name__}: {e}"[:300]}
     Mo, No = I1.shape
@@ -520,7 +520,7 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
 TRACK_ITS = 60  # iterations of the per-iteration divergence record (parity gate)
 
 
-def literal_engine_leg(args, rank, barrier, opts, I1, I2, flo, unk, gate_its, device):
+def literal_engine_leg(args, rank, opts, I1, I2, flo, unk, gate_its, device):
     """The literal-order engine (options arith="literal": every expression of
     gqmap_gpu_mixture.m:87-182 in the reference's own order, k_iter_lit) on
     the same pair, seed and steps: timed like the headline (settled clocks,
@@ -541,10 +541,12 @@ def literal_engine_leg(args, rank, barrier, opts, I1, I2, flo, unk, gate_its, de
         if not args.no_settle:
             settle_clocks(chunk, 20)
         eng.init_state(seed=rank)
-        barrier()
+        eng.synchronize()
+        # rank-local timing (the leg is reported from rank 0): no collective
+        # here, so a rank whose leg fails cannot leave the others waiting
         t0 = time.perf_counter()
         done, _ = eng.run(args.steps)
-        barrier()
+        eng.synchronize()
         elapsed = time.perf_counter() - t0
         mp = eng.map()
         eng.init_state(seed=rank)
