@@ -81,6 +81,7 @@ __device__ __forceinline__ float gq_sqrt_dev(float x)
 #define GQ_PRAGMA_UNROLL(n) _Pragma(GQ_STR2(unroll n))
 #define GQ_UNROLL2 GQ_PRAGMA_UNROLL(GQ_EDGE_UNROLL_N)
 #define GQ_PAIR_UNROLL GQ_PRAGMA_UNROLL(GQ_PAIR_UNROLL_N)
+#define GQ_PAIR_UNROLL_K(n) GQ_PRAGMA_UNROLL(n)
 #define GQ_NODE_UNROLL GQ_PRAGMA_UNROLL(GQ_NODE_UNROLL_N)
 #define GQ_UNROLL_FULL _Pragma("unroll")
 #define GQ_UMUL24(a, b) __umul24((uint32_t)(a), (uint32_t)(b))
@@ -252,12 +253,13 @@ __device__ __forceinline__ f2v sqrt2_pk(f2v x)
     return r;
 }
 
-template <typename TP>
+template <int PU, typename TP>
 __device__ __forceinline__ Sums<float> edge_sums_pk(TP tab, int k0, int K2, int dk, float eps, const EdgeCoef<float> &c)
 {
     f2v s0a = {0.f, 0.f}, sij = {0.f, 0.f}, smx = {0.f, 0.f};  // (s0, sa), (sxi, sxj), (sm, sx)
     const int np = K2 >> 1;
-    GQ_PAIR_UNROLL
+    constexpr int U = PU ? PU : GQ_PAIR_UNROLL_N;
+    GQ_PRAGMA_UNROLL(U)
     for (int k = k0; k < np; k += dk) {
         const float p = fma(c.A, tab[tab_at(T_XI, k)], c.B * tab[tab_at(T_XJ, k)]);
         const f2v d = f2v{c.C, c.C} + f2v{p, -p};  // C + p, C - p
@@ -277,13 +279,14 @@ __device__ __forceinline__ Sums<float> edge_sums_pk(TP tab, int k0, int K2, int 
     return S;
 }
 
-template <typename R, typename TP>
+// PU: mirror pairs per loop trip (0: GQ_PAIR_UNROLL_N)
+template <int PU = 0, typename R, typename TP>
 __device__ __forceinline__ Sums<R> edge_sums_dev(TP tab, int k0, int K2, int dk, R eps, const EdgeCoef<R> &c)
 {
     if constexpr (sizeof(R) == 4 && GQ_EDGE_PK)
-        return edge_sums_pk(tab, k0, K2, dk, eps, c);
+        return edge_sums_pk<PU>(tab, k0, K2, dk, eps, c);
     else
-        return edge_sums(tab, k0, K2, dk, eps, c);
+        return edge_sums<PU>(tab, k0, K2, dk, eps, c);
 }
 
 // Combine the Q partial quadrature sums of a node's lane group (adjacent
@@ -971,7 +974,12 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                     g = lit_edge_grad(tab, K2, P.epsn, P.lams, P.guard != 0, T, a, jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
                 } else {
                     const EdgeCoef<R> c = edge_coef(jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
-                    Sums<R> S = edge_sums_dev(tab, kj, K2, QA, P.epsn, c);
+                    // 4 mirror pairs per trip at Q = 1 for the fp32 mixture and
+                    // the fp64 ctf levels (profiles/r05_unroll_knobs.txt), else 2
+                    // (fp32 ctf: 130 VGPRs, 4 -> 3 waves per SIMD)
+                    constexpr int PU = QA == 1 && ((sizeof(R) == 4 && ENG == 0) || (sizeof(R) == 8 && ENG == 2))
+                                           ? GQ_PAIR_UNROLL_Q1 : 0;
+                    Sums<R> S = edge_sums_dev<PU>(tab, kj, K2, QA, P.epsn, c);
                     if (QA > 1) S = lane_combine<QA>(S);
                     g = edge_epi(S, c, P.lams, P.guard != 0, T, a, jb.o1, jb.o2, jb.p, ENG == 2);
                 }

@@ -14,8 +14,8 @@
 //     not depend on the order in which tiles, waves or threads add them.
 //
 // The includer defines GQ_HD (e.g. `__device__ __forceinline__` or `inline`),
-// GQ_SQRT(x) for double and float, GQ_UNROLL2, GQ_NODE_UNROLL and GQ_UNROLL_FULL
-// (loop-unroll pragmas or nothing), makes fma/fmin/fmax/floorf/fminf/fmaxf visible for float and double, then includes
+// GQ_SQRT(x) for double and float, GQ_UNROLL2, GQ_NODE_UNROLL, GQ_UNROLL_FULL and
+// GQ_PAIR_UNROLL_K(n) (loop-unroll pragmas or nothing), makes fma/fmin/fmax/floorf/fminf/fmaxf visible for float and double, then includes
 // this file.
 //
 // Reference lines this arithmetic restates: node_pot / edge_pot
@@ -617,12 +617,19 @@ struct Sums {
 // (k = (K^2-1)/2, xi = xj = 0) when K is odd.  Lane j of Q takes the pairs
 // k = j, j+Q, ... in increasing k and, if (npairs - j) % Q == 0, the centre
 // last.  body_pair(k) / body_center(k) do the evaluation and accumulation.
-template <typename FP, typename FC>
+// PU: pairs per loop trip (0: the includer's GQ_PAIR_UNROLL; the order of
+// the sums is the same for every PU).
+template <int PU = 0, typename FP, typename FC>
 GQ_HD void quad_pairs(int k0, int K2, int dk, FP body_pair, FC body_center)
 {
     const int np = K2 >> 1;
-    GQ_PAIR_UNROLL
-    for (int k = k0; k < np; k += dk) body_pair(k);
+    if constexpr (PU == 0) {
+        GQ_PAIR_UNROLL
+        for (int k = k0; k < np; k += dk) body_pair(k);
+    } else {
+        GQ_PAIR_UNROLL_K(PU)
+        for (int k = k0; k < np; k += dk) body_pair(k);
+    }
     if ((K2 & 1) && np >= k0 && (np - k0) % dk == 0) body_center(np);
 }
 
@@ -722,11 +729,11 @@ GQ_HD EdgeCoef<R> edge_coef(R u1, R u2, R o1, R o2, R p)
     c.C = u1 - u2;
     return c;
 }
-template <typename R, typename TP>
+template <int PU = 0, typename R, typename TP>
 GQ_HD Sums<R> edge_sums(TP tab, int k0, int K2, int dk, R eps, const EdgeCoef<R> &c)
 {
     Sums<R> S;
-    quad_pairs(
+    quad_pairs<PU>(
         k0, K2, dk,
         [&](int k) {
             // d = C +- p with p = A xi + B xj

@@ -19,6 +19,7 @@
 #define GQ_SQRT(x) sqrt(x)
 #define GQ_UNROLL2
 #define GQ_PAIR_UNROLL
+#define GQ_PAIR_UNROLL_K(n)
 #define GQ_NODE_UNROLL
 #define GQ_UNROLL_FULL 
 #include "gqmap_math.h"

@@ -13,6 +13,12 @@
 #ifndef GQ_PAIR_UNROLL_N
 #define GQ_PAIR_UNROLL_N 2
 #endif
+// ... at one lane per node for fp32 and the ctf levels (round 5,
+// profiles/r05_unroll_knobs.txt: 4 gains 2.4% on C2 fp32 and 0.8% on the
+// 480x640 level; fp64 C2 stays at 2)
+#ifndef GQ_PAIR_UNROLL_Q1
+#define GQ_PAIR_UNROLL_Q1 4
+#endif
 // Node quadrature: points per loop trip (r03_small_node_unroll: 1 is best)
 #ifndef GQ_NODE_UNROLL_N
 #define GQ_NODE_UNROLL_N 1

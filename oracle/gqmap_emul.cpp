@@ -33,6 +33,7 @@ using std::fmin;
 #define GQ_SQRT(x) std::sqrt(x)
 #define GQ_UNROLL2
 #define GQ_PAIR_UNROLL
+#define GQ_PAIR_UNROLL_K(n)
 #define GQ_NODE_UNROLL
 #define GQ_UNROLL_FULL
 #include "../gqmap-opticalflow_amd/csrc/gqmap_math.h"
