@@ -974,7 +974,10 @@ def main():
             # per pixel: node 2 x K x 6 flop, edges 4 x K^2 x ~40 flop (legacy/gqmap_cpu.m:20-54)
             fl = (2 * K * 6 + 4 * K * K * 40) * r["pixels"] * r["its"]
             out["roofline"] = {"bound": "valu", "achieved": fl / elapsed / 1e12, "peak": PEAK_TFLOPS["fp64"],
-                               "unit": "TFLOP/s", "frac": fl / elapsed / 1e12 / PEAK_TFLOPS["fp64"], "traffic": None,
+                               "unit": "TFLOP/s", "frac": fl / elapsed / 1e12 / PEAK_TFLOPS["fp64"],
+                               "traffic": traffic_per_launch("fp64", "c1"),
+                               "traffic_unit": "HBM bytes per iteration (grad + update + ctl)",
+                               "traffic_source": traffic_source("fp64", "c1"),
                                "kernel": "gq::k_legacy_grad + k_legacy_update + k_legacy_ctl (timed by the device call's wall "
                                          "clock)"}
         elif cfg == "c3":

@@ -8,6 +8,7 @@ known byte counts; WRITE_SIZE likewise.
 usage: python3 scripts/pmc_summary.py gpurun_out/<tag> <cfg> <prec>"""
 import csv
 import json
+import re
 import os
 import shutil
 import sys
@@ -68,10 +69,19 @@ def main():
         lines.append(f"{name[:70]:70s} {r['Calls']:>6s} {float(r['AverageNs']) / 1e3:10.2f} "
                      f"{f if f is not None else float('nan'):12.1f} {w if w is not None else float('nan'):12.1f} "
                      f"{(corr or float('nan')) / 1e6:13.3f}")
-        if "k_iter" in name and traffic is None and corr is not None:
+        if cfg != "c1" and "k_iter" in name and traffic is None and corr is not None:
             traffic = dict(kernel=name, avg_us=float(r["AverageNs"]) / 1e3, fetch_kb=f, write_kb=w,
                            fetch_corr=fcorr, write_corr=wcorr, hbm_bytes_per_launch=corr,
                            source=f"profiles/{tag}_{cfg}_{prec}_summary.txt")
+        if cfg == "c1" and "k_legacy" in name and "sigma0" not in name and corr is not None:
+            # C1: one iteration = k_legacy_grad + k_legacy_update + k_legacy_ctl
+            if traffic is None:
+                traffic = dict(kernel="k_legacy_grad + k_legacy_update + k_legacy_ctl (bytes per iteration)",
+                               avg_us=0.0, fetch_corr=fcorr, write_corr=wcorr, hbm_bytes_per_launch=0.0,
+                               per_kernel={}, source=f"profiles/{tag}_{cfg}_{prec}_summary.txt")
+            traffic["avg_us"] += float(r["AverageNs"]) / 1e3
+            traffic["hbm_bytes_per_launch"] += corr
+            traffic["per_kernel"][re.search(r"k_legacy_\w+", name).group(0)] = corr
     txt = "\n".join(lines) + "\n"
     open(os.path.join(ROOT, "profiles", f"{tag}_{cfg}_{prec}_summary.txt"), "w").write(txt)
     if traffic:
