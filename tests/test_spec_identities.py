@@ -82,3 +82,53 @@ def test_last_cell_identity():
                 b = O.emu_sample(VV, Mo, No, X, Y, fp32=fp32, cap=True)
                 assert np.all(np.isfinite(a))
                 np.testing.assert_array_equal(a, b)
+
+
+def _fma(a: float, b: float, c: float) -> float:
+    """IEEE fused multiply-add: the exact a*b + c rounded once (float() of a
+    Fraction is correctly rounded)."""
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def test_div_rcp_is_correctly_rounded():
+    # gqmap_math.h div_rcp (literal mode, device): with r = RN(1/y),
+    # q = RN(x r), q = RN(q + RN(x - q y) r) twice, equals RN(x/y) -- here for
+    # the literal engine's operands: x = XI^2 - XJ^2 of Gauss-Hermite nodes
+    # (|x| < 64), y = sqrtpr = sqrt(1 - p^2) with |p| <= corr_tor < 1.
+    rng = np.random.default_rng(5)
+    xs = list(rng.uniform(-60.0, 60.0, 3000)) + list(rng.uniform(-1e-3, 1e-3, 500)) + [0.0, 1.0, -1.0, 59.999]
+    ys = list(np.sqrt(1 - rng.uniform(-0.999, 0.999, 3000) ** 2)) + [1.0, 0.5, math.sqrt(1 - 0.999 ** 2)]
+    bad = 0
+    for i, x in enumerate(xs):
+        y = float(ys[i % len(ys)])
+        r = 1.0 / y
+        q = x * r
+        q = _fma(_fma(-q, y, x), r, q)
+        q = _fma(_fma(-q, y, x), r, q)
+        bad += q != x / y
+    assert bad == 0
+
+
+def test_legacy_df2_sums_are_exact_negations():
+    # gqmap_legacy.hip k_legacy_grad: the reference's c2 += df2 (df2 = -df1)
+    # chain, from +0, equals 0 - (the c1 += df1 chain) bit for bit -- zero
+    # terms of either sign and exact cancellations included -- so s2 = 0 - s1
+    # (legacy/gqmap_cpu.m:40-53).
+    rng = np.random.default_rng(9)
+    for trial in range(400):
+        n = int(rng.integers(1, 40))
+        df1 = list(rng.normal(0, 10.0 ** rng.integers(-8, 3), n))
+        for j in range(n):  # zeros of both signs and exact cancellations
+            u = rng.random()
+            if u < 0.15:
+                df1[j] = 0.0
+            elif u < 0.3:
+                df1[j] = -0.0
+            elif u < 0.4 and j > 0:
+                df1[j] = -df1[j - 1]
+        c1 = 0.0
+        c2 = 0.0
+        for d in df1:
+            c1 += d
+            c2 += -d
+        assert math.copysign(1.0, c2) == math.copysign(1.0, 0.0 - c1) and c2 == 0.0 - c1, (trial, df1)
