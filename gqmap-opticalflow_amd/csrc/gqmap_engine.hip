@@ -1080,9 +1080,12 @@ __device__ __forceinline__ void k_iter_body(const IterParams<R, VT> &P)
     const int tl = idle ? 0 : tile_of_block(bt, nb, P.cu_group, P.cu_slots, P.band_rows ? P.tiles_m : 0);
     const int tile = tl < P.seg_n[0] ? P.seg_lo[0] + tl : P.seg_lo[1] + (tl - P.seg_n[0]);
     // workgroups that start on one CU are local blocks j, j+S, j+2S of the
-    // XCD (see tile_of_block): alternate the phase order among them.  Not
-    // for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
-    const bool edge_first = GQ_PHASE_MIX && ENG != 1 && (((b >> 3) / P.cu_slots) & 1);
+    // XCD (see tile_of_block): alternate the phase order among them (node,
+    // edge, node first; the ctf levels at Q = 1 edge, node, edge: 480x640
+    // -2.7%, against +4.6% on C2 and +34% on C2 fp32, profiles/r05_phase_mix_inv.txt).
+    // Not for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
+    constexpr int INV = ENG == 2 && Q == 1 ? GQ_PHASE_MIX_CTF_Q1_INV : 0;
+    const bool edge_first = GQ_PHASE_MIX && ENG != 1 && ((((b >> 3) / P.cu_slots) & 1) != INV);
     __shared__ TileLdsQ<R, Q> lds;
     const int part_r = P.part_off + b;
     if (idle) {

@@ -39,6 +39,11 @@
 #ifndef GQ_PHASE_MIX
 #define GQ_PHASE_MIX 1
 #endif
+// ... with the order flipped (co-resident blocks j, j+S, j+2S: edge, node,
+// edge) on the ctf Q = 1 kernel (profiles/r05_phase_mix_inv.txt)
+#ifndef GQ_PHASE_MIX_CTF_Q1_INV
+#define GQ_PHASE_MIX_CTF_Q1_INV 1
+#endif
 // Waves per SIMD the register allocation must allow (MI355X: 136-168 VGPRs
 // -> 3, 176-256 -> 2).  Left to the allocator: forcing 3 waves on the
 // single-scale engine moved arrays to scratch (C2 +24%); bounding the super
