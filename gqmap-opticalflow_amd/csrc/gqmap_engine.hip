@@ -974,11 +974,15 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
                     g = lit_edge_grad(tab, K2, P.epsn, P.lams, P.guard != 0, T, a, jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
                 } else {
                     const EdgeCoef<R> c = edge_coef(jb.u1, jb.u2, jb.o1, jb.o2, jb.p);
-                    // 4 mirror pairs per trip at Q = 1 for the fp32 mixture and
-                    // the fp64 ctf levels (profiles/r05_unroll_knobs.txt), else 2
-                    // (fp32 ctf: 130 VGPRs, 4 -> 3 waves per SIMD)
-                    constexpr int PU = QA == 1 && ((sizeof(R) == 4 && ENG == 0) || (sizeof(R) == 8 && ENG == 2))
-                                           ? GQ_PAIR_UNROLL_Q1 : 0;
+                    // 4 mirror pairs per trip at Q = 1 for the fp32 mixture, the
+                    // fp64 ctf levels and the non-temporal (large-frame, C5)
+                    // kernels with float taps (profiles/r05_unroll_knobs.txt,
+                    // r05_c5_variants.txt), else 2 (fp32 ctf: 130 VGPRs and the
+                    // double-tap mixture NT kernel 170: 3 -> 2 waves per SIMD)
+                    constexpr int PU =
+                        QA == 1 && ((sizeof(R) == 4 && ENG == 0) ||
+                                    (sizeof(R) == 8 && (ENG == 2 || (NT && sizeof(VT) == 4))))
+                            ? GQ_PAIR_UNROLL_Q1 : 0;
                     Sums<R> S = edge_sums_dev<PU>(tab, kj, K2, QA, P.epsn, c);
                     if (QA > 1) S = lane_combine<QA>(S);
                     g = edge_epi(S, c, P.lams, P.guard != 0, T, a, jb.o1, jb.o2, jb.p, ENG == 2);
@@ -1084,7 +1088,7 @@ __device__ __forceinline__ void k_iter_body(const IterParams<R, VT> &P)
     // edge, node first; the ctf levels at Q = 1 edge, node, edge: 480x640
     // -2.7%, against +4.6% on C2 and +34% on C2 fp32, profiles/r05_phase_mix_inv.txt).
     // Not for the super engine, whose node phase dominates (C4: 850 vs 680 us/it).
-    constexpr int INV = ENG == 2 && Q == 1 ? GQ_PHASE_MIX_CTF_Q1_INV : 0;
+    constexpr int INV = ENG == 2 && Q == 1 ? GQ_PHASE_MIX_CTF_Q1_INV : GQ_PHASE_MIX_OTHER_INV;
     const bool edge_first = GQ_PHASE_MIX && ENG != 1 && ((((b >> 3) / P.cu_slots) & 1) != INV);
     __shared__ TileLdsQ<R, Q> lds;
     const int part_r = P.part_off + b;

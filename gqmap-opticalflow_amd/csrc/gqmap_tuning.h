@@ -44,6 +44,9 @@
 #ifndef GQ_PHASE_MIX_CTF_Q1_INV
 #define GQ_PHASE_MIX_CTF_Q1_INV 1
 #endif
+#ifndef GQ_PHASE_MIX_OTHER_INV  // the other single-pixel kernels
+#define GQ_PHASE_MIX_OTHER_INV 0
+#endif
 // Waves per SIMD the register allocation must allow (MI355X: 136-168 VGPRs
 // -> 3, 176-256 -> 2).  Left to the allocator: forcing 3 waves on the
 // single-scale engine moved arrays to scratch (C2 +24%); bounding the super
