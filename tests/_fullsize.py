@@ -23,6 +23,9 @@ CONFIGS = {
     "c2": dict(name="rubberwhale", engine="mixture", L=1, K=9),
     "c3": dict(name="Grove3", engine="ctf", L=1, K=11),
     "c4": dict(name="Urban3", engine="super", L=3, K=11),
+    # the other 584x388 pairs of the multi-GPU frame-parallel runs (bench.PAIRS)
+    "c2_dimetrodon": dict(name="Dimetrodon", engine="mixture", L=1, K=9),
+    "c2_hydrangea": dict(name="Hydrangea", engine="mixture", L=1, K=9),
 }
 
 

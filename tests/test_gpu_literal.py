@@ -60,6 +60,18 @@ def test_c2_literal_engine_bit_exact_vs_restatement(its):
     np.testing.assert_array_equal(flow_to_color(mp)[0], oracle.flow_to_color(omap)[0])
 
 
+@pytest.mark.parametrize("cfg,init", [("c2", "tight"), ("c2_dimetrodon", "ref"), ("c2_hydrangea", "tight")])
+def test_literal_engine_other_pairs_and_states_bit_exact(cfg, init):
+    # the same bar on the other 584x388 pairs and from a converging state
+    # (mu near the ground truth: most samples interior), 20 iterations
+    I1, I2, flo, unk, o, st = F.case(cfg, init)
+    done, tr, g, mp = _gpu_lit(o, I1, I2, st, 20)
+    odone, otr, ost = _oracle(o, I1, I2, st, 20)
+    assert done == odone == 20
+    _same(g, ost)
+    np.testing.assert_allclose(tr, otr, rtol=1e-12)
+
+
 def test_literal_engine_tiles_bit_exact_vs_whole_grid():
     # the in-process strip transport (ghost columns, exact totals) in literal mode
     from gqmap_opticalflow_amd import Engine, tile_group_run
