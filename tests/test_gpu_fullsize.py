@@ -90,3 +90,13 @@ def test_c4_workload_compressed_schedule_bit_exact(mode):
     assert g.T == e[2] == pytest.approx(0.2 * 0.75 ** 3)
     assert not np.array_equal(g.alpha, st.alpha)  # the alpha update ran
     assert g.alpha.sum() == pytest.approx(1.0)
+
+
+@pytest.mark.parametrize("cfg", ["c2_dimetrodon", "c2_hydrangea"])
+def test_fullsize_other_pairs_20_iterations_bit_exact(cfg):
+    # the frames the multi-GPU frame-parallel ranks solve (bench.PAIRS):
+    # 20 fp64 iterations bit-identical to the CPU model
+    I1, I2, _, _, o, st = F.case(cfg, "ref")
+    done, tr, g, split = _gpu(o, I1, I2, st, 20)
+    assert split == 1
+    _bit_exact(g, tr, done, _emu(o, I1, I2, st, 20, split))
