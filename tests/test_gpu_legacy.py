@@ -107,3 +107,23 @@ def test_legacy_device_arrays_rejects_host_and_row_major():
     rc = load().gqmap_cpu_run_device(C.byref(o), flow.ctypes.data, 8, 9, None, C.c_uint64(0),
                                      *[a.ctypes.data for a in out], None, None, 0)
     assert rc != 0
+
+
+@pytest.mark.parametrize("name", ["Hydrangea", "rubberwhale"])
+def test_legacy_other_pairs_device_arrays_bit_exact(name):
+    """C1's 50 iterations on the other 584x388 GT flows, through the
+    device-array entry point, against the C restatement."""
+    import torch
+    from gqmap_opticalflow_amd import flow_to_color, flowio, gauss_hermite, gqmap_cpu_device, rand_uniform
+    from oracle import oracle
+    gt = flowio.load_pair(name)[2]
+    _, flo, _, unk = flow_to_color(gt)
+    M, N, _ = flo.shape
+    sg0 = np.asfortranarray(rand_uniform(0, 3, 2 * M * N).reshape((M, N, 2), order="F") + 2)
+    o = dict(its=50, K=9)
+    mu, sg, rou, tr = gqmap_cpu_device(o, torch.from_numpy(np.asfortranarray(flo)).to("cuda:0"), seed=0,
+                                       return_trace=True)
+    X, W = gauss_hermite(9)
+    r = oracle.cpu_run(o, flo, sg0, X, W, nthreads=min(16, os.cpu_count() or 1))
+    for a, b, k in zip((mu, sg, rou, tr), r, ("mu", "sigma", "rou", "trace")):
+        np.testing.assert_array_equal(a.cpu().numpy(), b, err_msg=k)
