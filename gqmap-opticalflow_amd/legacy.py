@@ -87,6 +87,10 @@ def gqmap_cpu_device(options: dict, flow, *, sigma0=None, seed: int = 0, return_
     mu, sigma, rou = _fortran_dev((M, N, 2), dev), _fortran_dev((M, N, 2), dev), _fortran_dev((M, N, 2, 2), dev)
     import torch
     trace = torch.empty((max(o.its, 1), 3), dtype=torch.float64, device=dev)
+    # the library runs on its own HIP runtime's queue: torch work that
+    # produced flow / sigma0 must have finished (the call itself returns
+    # synchronised)
+    torch.cuda.synchronize(dev)
     done = C.c_int(0)
     check(_lib.load().gqmap_cpu_run_device(C.byref(o), flow.data_ptr(), M, N,
                                            sigma0.data_ptr() if sigma0 is not None else None, C.c_uint64(seed),
