@@ -772,7 +772,7 @@ def tiled_solve(args, rank, world, local, barrier, dist, I1, I2, flo, unk, opts,
         mp = eng.map()
         col0, col1 = eng.col0, eng.col1
         # k_iter durations: a replay of the same iterations with HIP events
-        # around the boundary + interior launches of every iteration
+        # around every iteration's k_iter launch over the strip
         eng.init_state(seed=0)
         done2, total_ms, kernel_ms = eng.run_timed(args.steps)
         if done2 != args.steps or not np.array_equal(eng.map(), mp):

@@ -19,7 +19,8 @@
 // remaining launches into no-ops.  (Normally the finalize is fused into the
 // last k_iter workgroup.  The smallest coarse-to-fine levels run a whole
 // chunk in one k_iter_persist launch; column-strip tiles over RCCL add the
-// ghost-column exchange and, for L = 1, finalize one iteration behind.)
+// ghost-column exchange and, for L = 1, all-gather and finalize the exact
+// totals once per 50-iteration sequence.)
 //
 // Layout: every field is a MATLAB column-major plane (m fastest).  A state
 // buffer is 9 planes of M*N*L: muu, muv, sigu, sigv, pn, rou(dir=1,u),
@@ -31,6 +32,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -1831,6 +1834,30 @@ hipError_t mixture_map_device(const double *alpha_host, const void *st, bool fp3
                               int M, int N, int L, double *out_dev, hipStream_t s);
 }
 
+// Execution policies that never change a result (placement, caching, launch
+// shape; tests/test_gpu_parity.py, test_gpu_persist.py hold them to the same
+// bits): chosen automatically, overridable only through the debug entry
+// gqmap_debug_policy (tests and A/B scripts; not in the public header).  The
+// library reads no environment variables.  A context copies the process-wide
+// setting when it is created (gqmap_ctx::pol) and reads only its copy, so a
+// later gqmap_debug_policy call never changes a context already running.
+namespace gq {
+struct Policy {
+    int nt_state = -1;     // non-temporal state stores: -1 auto (state > 32 MiB), 0 off, 1 on
+    int band_rows = -1;    // row-by-row walk of each XCD's band: -1 auto (padded VV > 4 MiB), 0, 1
+    int cu_group = -1;     // co-resident tile grouping: -1 from the occupancy query, 0 off, n > 0 forced
+    int lpar = -1;         // super engine L > 1: -1 one block per (tile, component), 1 one block per tile
+    int lpar_xcd = 1;      // a tile's component blocks on one XCD (whole-grid fused launch)
+    int fused_finalize = 1;
+    int persist = 1;       // persistent launch of the small ctf levels
+    int persist_cap = -1;  // resident workgroups assumed by the persistent launch (-1: occupancy query)
+    int graph = 1;         // replayed hipGraphs (0: direct launches)
+    int vv_float = 1;      // float padded-frame store when exact
+    int verbose = 0;       // recovery messages on stderr
+};
+Policy g_pol;
+}  // namespace gq
+
 struct gqmap_ctx {
     gqmap_options opt;
     int device = 0;
@@ -1897,29 +1924,9 @@ struct gqmap_ctx {
     fix128 *d_rows = nullptr, *d_seqg = nullptr;
     fix128 *seq_row = nullptr;  // the row of the iteration being issued
     bool spec_now = false;      // the launches being issued run by Ctl::it_i / done_i / T_i
+    gq::Policy pol = gq::g_pol;  // execution policies, fixed at creation
 };
 
-// Execution policies that never change a result (placement, caching, launch
-// shape; tests/test_gpu_parity.py, test_gpu_persist.py hold them to the same
-// bits): chosen automatically, overridable only through the debug entry
-// gqmap_debug_policy (tests and A/B scripts; not in the public header).  The
-// library reads no environment variables.
-namespace gq {
-struct Policy {
-    int nt_state = -1;     // non-temporal state stores: -1 auto (state > 32 MiB), 0 off, 1 on
-    int band_rows = -1;    // row-by-row walk of each XCD's band: -1 auto (padded VV > 4 MiB), 0, 1
-    int cu_group = -1;     // co-resident tile grouping: -1 from the occupancy query, 0 off, n > 0 forced
-    int lpar = -1;         // super engine L > 1: -1 one block per (tile, component), 1 one block per tile
-    int lpar_xcd = 1;      // a tile's component blocks on one XCD (whole-grid fused launch)
-    int fused_finalize = 1;
-    int persist = 1;       // persistent launch of the small ctf levels
-    int persist_cap = -1;  // resident workgroups assumed by the persistent launch (-1: occupancy query)
-    int graph = 1;         // replayed hipGraphs (0: direct launches)
-    int vv_float = 1;      // float padded-frame store when exact
-    int verbose = 0;       // recovery messages on stderr
-};
-Policy g_pol;
-}  // namespace gq
 
 namespace {
 
@@ -1960,10 +1967,10 @@ int choose_split(int M, int N, int L, int forced, bool super_, bool ctf)
 // Components per k_iter block: the super engine's node grid is 16x smaller
 // than the frame, so its L components run as separate blocks (more
 // workgroups, fewer lanes per node).  Sums are exact fixed point: the split
-// never changes results.  GQMAP_LPAR=1 forces one block per tile.
+// never changes results.  Policy lpar = 1 forces one block per tile.
 int choose_lpar(const gqmap_ctx *c)
 {
-    if (g_pol.lpar == 1) return 1;
+    if (c->pol.lpar == 1) return 1;
     return c->super_ && c->L > 1 ? c->L : 1;
 }
 
@@ -2057,8 +2064,9 @@ void tile_segments(const gqmap_ctx *c, TileSegs &bnd, TileSegs &inr)
     // Q = 64, of a strip with a left neighbour): never launched
 }
 
-// Workgroups of one RCCL-tile iteration (the boundary and the interior
-// launch): the count the last-arrival ticket of tile_totals_tail waits for.
+// Workgroups of one RCCL-tile iteration (its one launch over the strip's
+// tiles, strip_launch): the count the last-arrival ticket of
+// tile_totals_tail waits for.
 // Not c->nblocks -- a ghost-only tile column is not launched.
 int iteration_blocks(const gqmap_ctx *c)
 {
@@ -2075,25 +2083,25 @@ FinParams fin_params(const gqmap_ctx *c);
 // together (8 x 4 MiB): it is streamed once per iteration and would evict
 // the frame's gather lines (C5 fetch 691 -> 582 MB per launch, time -0.4%);
 // a C2-sized buffer (16 MB) is partly still in L2 when the next iteration
-// reads it (round 3: NT stores on C2 +0.8%).  GQMAP_NT_STATE=0/1 forces.
+// reads it (round 3: NT stores on C2 +0.8%).  Policy nt_state = 0/1 forces.
 bool state_nt(const gqmap_ctx *c)
 {
-    if (g_pol.nt_state >= 0) return g_pol.nt_state == 1;
+    if (c->pol.nt_state >= 0) return c->pol.nt_state == 1;
     return (size_t)c->MNL * NPLANES * c->rsz > ((size_t)32 << 20);
 }
 
 // Row-by-row tile walk within each XCD's band (tile_of_block) for frames
-// whose padded VV is larger than one XCD's 4 MiB L2.  GQMAP_BAND_ROWS=0/1 forces.
+// whose padded VV is larger than one XCD's 4 MiB L2.  Policy band_rows = 0/1 forces.
 bool band_rows(const gqmap_ctx *c)
 {
-    if (g_pol.band_rows >= 0) return g_pol.band_rows == 1;
+    if (c->pol.band_rows >= 0) return c->pol.band_rows == 1;
     const size_t vsz = c->fp32 ? sizeof(float) : c->vv32 ? sizeof(vvs_t) : sizeof(double);
     return vv_elems(c->Mo, c->No) * vsz > ((size_t)4 << 20);
 }
 
 bool fused_finalize(const gqmap_ctx *c)
 {
-    return c->nranks == 0 && g_pol.fused_finalize;
+    return c->nranks == 0 && c->pol.fused_finalize;
 }
 
 template <typename R, typename VT>
@@ -2189,11 +2197,11 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
         if (nblocks == 0) return;
     }
     static const int2 shape = kernel_shape(k_iter<R, VT, ENG, Q>);
-    if (g_pol.cu_group != 0) {
-        P.cu_group = g_pol.cu_group > 0 ? g_pol.cu_group : shape.x;
+    if (c->pol.cu_group != 0) {
+        P.cu_group = c->pol.cu_group > 0 ? c->pol.cu_group : shape.x;
         P.cu_slots = std::max(1, shape.y / 8);
     }
-    if (c->lpar > 1 && P.fused && !sg && g_pol.lpar_xcd) {
+    if (c->lpar > 1 && P.fused && !sg && c->pol.lpar_xcd) {
         P.lpar_xcd = 1;
         nblocks = 8 * c->lpar * ((c->tiles_m * c->tiles_n + 7) / 8);
     }
@@ -2284,9 +2292,9 @@ void launch_finalize(gqmap_ctx *c) { k_finalize<<<1, 256, 0, c->stream>>>(fin_pa
 // ---- persistent small-grid launches (k_iter_persist) ------------------------
 // Whole-grid ctf contexts with L = 1 and Q >= 8 (grids below 2^13 nodes)
 // whose tiles plus the finalizer fit the device's resident workgroups
-// (GQMAP_NO_PERSIST=1: one launch per iteration instead).
+// (the context's policy persist = 0: one launch per iteration instead).
 template <typename R, typename VT, int Q>
-int persist_capacity()
+int persist_capacity(const gqmap_ctx *c)
 {
     static int cap = -1;
     if (cap < 0) {
@@ -2306,7 +2314,7 @@ int persist_capacity()
     }
     // policy persist_cap: resident workgroups assumed (tests force the
     // per-iteration path with a capacity too small for the grid)
-    return g_pol.persist_cap >= 0 ? g_pol.persist_cap : cap;
+    return c->pol.persist_cap >= 0 ? c->pol.persist_cap : cap;
 }
 
 // The snapshot buffers of the persistent path (allocated outside a capture;
@@ -2334,7 +2342,7 @@ template <typename R, typename VT, int Q>
 bool launch_persist_q(gqmap_ctx *c, int n, bool dry)
 {
     const int G = c->nblocks;
-    if (G + 1 > persist_capacity<R, VT, Q>()) return false;
+    if (G + 1 > persist_capacity<R, VT, Q>(c)) return false;
     if (!ensure_snap(c)) return false;
     if (dry) return true;
     {
@@ -2349,7 +2357,7 @@ bool launch_persist_q(gqmap_ctx *c, int n, bool dry)
     P.fin.nblocks = 2 * G;  // partial row stride: iteration j writes rows (j & 1) * G + b
     const int threads = Q == 64 ? WN_THREADS : BLOCK;
     static const int2 shape = kernel_shape(k_iter_persist<R, VT, 2, Q>);
-    P.cu_group = Q == 64 || g_pol.cu_group == 0 ? 1 : g_pol.cu_group > 0 ? g_pol.cu_group : shape.x;
+    P.cu_group = Q == 64 || c->pol.cu_group == 0 ? 1 : c->pol.cu_group > 0 ? c->pol.cu_group : shape.x;
     P.cu_slots = std::max(1, shape.y / 8);
     k_iter_persist<R, VT, 2, Q><<<G + 1, threads, 0, c->stream>>>(P, n);
     return true;
@@ -2375,7 +2383,7 @@ bool launch_persist_t(gqmap_ctx *c, int n, bool dry)
 // dry: only the check
 bool launch_persist(gqmap_ctx *c, int n, bool dry = false)
 {
-    if (!g_pol.persist || c->persist_off || c->opt.engine != GQMAP_ENGINE_CTF || c->L != 1 || c->n_tiles != 1 || c->comm || c->nranks != 0 ||
+    if (!c->pol.persist || c->persist_off || c->opt.engine != GQMAP_ENGINE_CTF || c->L != 1 || c->n_tiles != 1 || c->comm || c->nranks != 0 ||
         !fused_finalize(c) || n < 1)
         return false;
     if (c->fp32) return launch_persist_t<float, float>(c, n, dry);
@@ -2435,12 +2443,188 @@ const Rccl *rccl()
 
 }  // namespace
 
+struct LoopGroup;
+
+// The communicator of an RCCL tile.  loop (tests only, never set by
+// gqmap_tile_attach_rccl): the in-process loopback transport below stands in
+// for the three NCCL calls of the strip iteration -- the grouped
+// ncclSend/ncclRecv of exchange_rccl and the two ncclAllGather of
+// launch_step_rccl / launch_seq_deferred -- so that n tile contexts, one host
+// thread each, run the multi-rank iteration's own code with real neighbours
+// on one GPU.
 struct RcclComm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0;
+    LoopGroup *loop = nullptr;
+};
+
+// Loopback transport (gqmap_debug_loop_*).  Each rank's thread posts its
+// buffers, records `ready` on its own stream after the work the collective
+// follows, and meets the others at a host barrier; then each rank enqueues,
+// on its own stream, a wait on every peer's `ready` and device copies of what
+// it receives (from the peer's send buffer into its receive buffer -- what
+// NCCL moves), records `done`, meets the others again and waits on the
+// `done` of every peer that read its buffers before its stream goes on (the
+// peer's copy must land before this rank's next pack overwrites the source:
+// NCCL's send completes only when the peer has the data).  The collectives
+// of all ranks are matched in issue order, as NCCL matches them; a peer whose
+// posted sizes do not match, or a barrier that times out (a rank left the
+// sequence), fails the call.
+struct LoopGroup {
+    struct P2p {
+        int peer;
+        const void *send;  // kind 0: send buffer to `peer`
+        void *recv;        // kind 0: receive buffer from `peer`
+        size_t bytes;
+    };
+    struct Post {
+        int kind = -1;  // 0: grouped send/recv, 1: all-gather
+        P2p sends[2], recvs[2];
+        int ns = 0, nr = 0;
+        const void *ag_send = nullptr;  // all-gather: this rank's block
+        void *ag_recv = nullptr;        // rank-major [nranks][bytes]
+        size_t ag_bytes = 0;
+    };
+    int n = 0, device = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    unsigned long long gen = 0;
+    bool broken = false;
+    std::vector<hipEvent_t> ready, done;
+    std::vector<Post> post;
+    unsigned long long calls = 0;  // collectives completed (rank 0's count)
 };
 
 namespace {
+
+// Host barrier of a loopback group; false: a rank did not arrive within the
+// time limit (it left the collective sequence) or the group is broken.
+bool loop_barrier(LoopGroup *g)
+{
+    std::unique_lock<std::mutex> lk(g->mu);
+    if (g->broken) return false;
+    const unsigned long long my = g->gen;
+    if (++g->arrived == g->n) {
+        g->arrived = 0;
+        ++g->gen;
+        g->cv.notify_all();
+        return true;
+    }
+    if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->gen != my || g->broken; }) || g->broken) {
+        g->broken = true;
+        g->cv.notify_all();
+        return false;
+    }
+    return true;
+}
+
+// One collective of rank r (see LoopGroup).
+gqmap_status loop_collective(gqmap_ctx *c, const LoopGroup::Post &mine)
+{
+    LoopGroup *g = c->comm->loop;
+    const int r = c->comm->rank;
+    GQ_HIP(hipEventRecord(g->ready[r], c->stream));
+    g->post[r] = mine;
+    GQ_CHECK(loop_barrier(g), GQMAP_ERR_HIP, "loopback transport: rank %d: a peer did not reach the collective", r);
+    std::vector<int> peers;  // ranks whose buffers this rank reads, or that read this rank's
+    gqmap_status st = GQMAP_OK;
+    for (int q = 0; q < g->n && st == GQMAP_OK; ++q)
+        if (g->post[q].kind != mine.kind) {
+            set_error("loopback transport: rank %d issued collective kind %d, rank %d kind %d", r, mine.kind, q,
+                      g->post[q].kind);
+            st = GQMAP_ERR_HIP;
+        }
+    if (st == GQMAP_OK && mine.kind == 0) {
+        for (int i = 0; i < mine.nr && st == GQMAP_OK; ++i) {
+            const LoopGroup::P2p &rv = mine.recvs[i];
+            const LoopGroup::Post &pp = g->post[rv.peer];
+            const LoopGroup::P2p *sd = nullptr;
+            for (int j = 0; j < pp.ns; ++j)
+                if (pp.sends[j].peer == r) sd = &pp.sends[j];
+            if (!sd || sd->bytes != rv.bytes) {
+                set_error("loopback transport: rank %d receives %zu bytes from rank %d, which sends %zu", r, rv.bytes,
+                          rv.peer, sd ? sd->bytes : (size_t)0);
+                st = GQMAP_ERR_HIP;
+                break;
+            }
+            if (hipStreamWaitEvent(c->stream, g->ready[rv.peer], 0) != hipSuccess ||
+                hipMemcpyAsync(rv.recv, sd->send, rv.bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+                st = GQMAP_ERR_HIP;
+            peers.push_back(rv.peer);
+        }
+        for (int i = 0; i < mine.ns; ++i) peers.push_back(mine.sends[i].peer);
+    } else if (st == GQMAP_OK) {
+        for (int q = 0; q < g->n && st == GQMAP_OK; ++q) {
+            const LoopGroup::Post &pp = g->post[q];
+            if (pp.ag_bytes != mine.ag_bytes) {
+                set_error("loopback transport: all-gather of %zu bytes on rank %d, %zu on rank %d", mine.ag_bytes, r,
+                          pp.ag_bytes, q);
+                st = GQMAP_ERR_HIP;
+                break;
+            }
+            char *dst = (char *)mine.ag_recv + (size_t)q * mine.ag_bytes;
+            if (q == r && dst == pp.ag_send) continue;  // in place
+            if ((q != r && hipStreamWaitEvent(c->stream, g->ready[q], 0) != hipSuccess) ||
+                hipMemcpyAsync(dst, pp.ag_send, mine.ag_bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+                st = GQMAP_ERR_HIP;
+            if (q != r) peers.push_back(q);
+        }
+    }
+    if (st == GQMAP_OK && hipEventRecord(g->done[r], c->stream) != hipSuccess) st = GQMAP_ERR_HIP;
+    if (st != GQMAP_OK) {  // release the peers waiting at the second barrier
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->broken = true;
+        g->cv.notify_all();
+        if (!gqmap_last_error()[0]) set_error("loopback transport: rank %d: HIP call failed", r);
+        return st;
+    }
+    GQ_CHECK(loop_barrier(g), GQMAP_ERR_HIP, "loopback transport: rank %d: a peer failed in the collective", r);
+    for (int q : peers) GQ_HIP(hipStreamWaitEvent(c->stream, g->done[q], 0));
+    if (r == 0) ++g->calls;
+    return GQMAP_OK;
+}
+
+// The ghost-column send/recv pairs of one iteration: grouped ncclSend /
+// ncclRecv with the neighbour ranks, or the loopback transport.
+gqmap_status comm_sendrecv(gqmap_ctx *c, const LoopGroup::P2p *sends, int ns, const LoopGroup::P2p *recvs, int nr,
+                           size_t elem)
+{
+    if (c->comm->loop) {
+        LoopGroup::Post p;
+        p.kind = 0;
+        p.ns = ns;
+        p.nr = nr;
+        for (int i = 0; i < ns; ++i) p.sends[i] = sends[i];
+        for (int i = 0; i < nr; ++i) p.recvs[i] = recvs[i];
+        return loop_collective(c, p);
+    }
+    const ncclDataType_t dt = elem == sizeof(float) ? ncclFloat : ncclDouble;
+    const Rccl *R = rccl();
+    GQ_NCCL(R->GroupStart());
+    for (int i = 0; i < std::max(ns, nr); ++i) {
+        if (i < ns) GQ_NCCL(R->Send(sends[i].send, sends[i].bytes / elem, dt, sends[i].peer, c->comm->comm, c->stream));
+        if (i < nr) GQ_NCCL(R->Recv(recvs[i].recv, recvs[i].bytes / elem, dt, recvs[i].peer, c->comm->comm, c->stream));
+    }
+    GQ_NCCL(R->GroupEnd());
+    return GQMAP_OK;
+}
+
+// All-gather of `bytes` per rank into the rank-major `recv` (in place when
+// send is this rank's block of recv): ncclAllGather, or the loopback transport.
+gqmap_status comm_allgather(gqmap_ctx *c, const void *send, void *recv, size_t bytes)
+{
+    if (c->comm->loop) {
+        LoopGroup::Post p;
+        p.kind = 1;
+        p.ag_send = send;
+        p.ag_recv = recv;
+        p.ag_bytes = bytes;
+        return loop_collective(c, p);
+    }
+    GQ_NCCL(rccl()->AllGather(send, recv, bytes, ncclUint8, c->comm->comm, c->stream));
+    return GQMAP_OK;
+}
 
 // sides: the present ones (left and/or right), one launch
 template <typename R>
@@ -2523,21 +2707,19 @@ gqmap_status exchange_rccl(gqmap_ctx *c)
     const int r = c->comm->rank;
     const bool left = c->tile > 0, right = c->tile < c->n_tiles - 1;
     if (!left && !right) return GQMAP_OK;
-    const size_t nl = (size_t)HALO_TO_LEFT_N * c->L * c->M, nr = (size_t)HALO_TO_RIGHT_N * c->L * c->M;
-    const ncclDataType_t dt = c->fp32 ? ncclFloat : ncclDouble;
-    const Rccl *R = rccl();
+    const size_t bl = (size_t)HALO_TO_LEFT_N * c->L * c->M * c->rsz, br = (size_t)HALO_TO_RIGHT_N * c->L * c->M * c->rsz;
     halo_pack(c, c->stream);
-    GQ_NCCL(R->GroupStart());
+    LoopGroup::P2p sd[2], rv[2];
+    int n = 0;
     if (left) {
-        GQ_NCCL(R->Send(c->d_halo[0], nl, dt, r - 1, c->comm->comm, c->stream));
-        GQ_NCCL(R->Recv(c->d_halo[2], nr, dt, r - 1, c->comm->comm, c->stream));
+        sd[n] = {r - 1, c->d_halo[0], nullptr, bl};
+        rv[n++] = {r - 1, nullptr, c->d_halo[2], br};
     }
     if (right) {
-        GQ_NCCL(R->Send(c->d_halo[1], nr, dt, r + 1, c->comm->comm, c->stream));
-        GQ_NCCL(R->Recv(c->d_halo[3], nl, dt, r + 1, c->comm->comm, c->stream));
+        sd[n] = {r + 1, c->d_halo[1], nullptr, br};
+        rv[n++] = {r + 1, nullptr, c->d_halo[3], bl};
     }
-    GQ_NCCL(R->GroupEnd());
-    return GQMAP_OK;
+    return comm_sendrecv(c, sd, n, rv, n, c->rsz);
 }
 
 // One exact iteration of an RCCL tile (L > 1, whose alpha update needs every
@@ -2558,8 +2740,8 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
     gqmap_status st = exchange_rccl(c);
     if (st != GQMAP_OK) return st;
     // (this rank's totals row was written by the launch's last workgroup: tile_totals_tail)
-    GQ_NCCL(rccl()->AllGather(c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128), ncclUint8,
-                              c->comm->comm, c->stream));
+    st = comm_allgather(c, c->d_gathered + (size_t)r * NP, c->d_gathered, (size_t)NP * sizeof(fix128));
+    if (st != GQMAP_OK) return st;
     unpack_finalize(c);  // received ghost columns + finalize, one launch
     return GQMAP_OK;
 }
@@ -2594,6 +2776,19 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
 bool deferred(const gqmap_ctx *c)
 {
     return c->comm && c->L == 1 && c->d_rows && c->d_snap && c->snap_bytes == (size_t)c->MNL * NPLANES * c->rsz;
+}
+
+// An L = 1 RCCL tile always runs deferred sequences: the snapshot follows
+// the grid size (a later gqmap_set_images may change it) and is allocated
+// here, outside any capture; failing that, the run fails on this rank --
+// never a quiet switch to the exact step, whose collectives would not match
+// the other ranks' sequences.
+gqmap_status comm_snap(gqmap_ctx *c)
+{
+    if (!c->comm || c->L != 1) return GQMAP_OK;
+    GQ_CHECK(c->d_rows && ensure_snap(c), GQMAP_ERR_HIP, "tile %d: deferred-sequence snapshot (%zu bytes) not allocated",
+             c->tile, (size_t)c->MNL * NPLANES * c->rsz);
+    return GQMAP_OK;
 }
 
 template <typename R>
@@ -2649,9 +2844,8 @@ gqmap_status launch_seq_deferred(gqmap_ctx *c, int n, hipEvent_t *ev = nullptr)
         gqmap_status st = launch_step_deferred(c, i, ev ? ev[2 * i] : nullptr, ev ? ev[2 * i + 1] : nullptr);
         if (st != GQMAP_OK) return st;
     }
-    const Rccl *R = rccl();
-    GQ_NCCL(R->AllGather(c->d_rows, c->d_seqg, (size_t)n * NP * sizeof(fix128), ncclUint8, c->comm->comm,
-                         c->stream));
+    gqmap_status st = comm_allgather(c, c->d_rows, c->d_seqg, (size_t)n * NP * sizeof(fix128));
+    if (st != GQMAP_OK) return st;
     k_finalize_seq<<<1, 256, 0, c->stream>>>(fin_params(c), c->d_seqg, n);
     return GQMAP_OK;
 }
@@ -2731,7 +2925,7 @@ gqmap_status persist_recover(gqmap_ctx *c, bool *recovered)
     GQ_HIP(hipMemcpyAsync(c->d_ctl, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToDevice, c->stream));
     GQ_HIP(hipMemsetAsync(c->d_bar, 0, sizeof(unsigned) * BAR_WORDS, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
-    if (g_pol.verbose)
+    if (c->pol.verbose)
         fprintf(stderr, "gqmap: persistent launch failed (%d workgroups); restored iteration %d, "
                         "continuing with one launch per iteration\n", c->nblocks + 1, h.it);
     c->persist_off = true;
@@ -2810,7 +3004,8 @@ gqmap_status capture_steps(gqmap_ctx *c, int n, hipGraphExec_t *out)
 {
     if (*out) return GQMAP_OK;
     (void)launch_persist(c, n, true);  // occupancy query, snapshot buffers: outside the capture
-    if (c->comm && c->L == 1) (void)ensure_snap(c);  // the deferred RCCL sequence's snapshot
+    gqmap_status st0 = comm_snap(c);  // the deferred RCCL sequence's snapshot
+    if (st0 != GQMAP_OK) return st0;
     hipGraph_t g;
     GQ_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     gqmap_status st = launch_steps(c, n);
@@ -2827,6 +3022,12 @@ gqmap_status capture_steps(gqmap_ctx *c, int n, hipGraphExec_t *out)
 }
 
 gqmap_status ensure_graph(gqmap_ctx *c) { return capture_steps(c, GRAPH_CHUNK, &c->graph); }
+
+// A loopback-transport tile (tests) runs its launches directly: its
+// collectives are host barriers and cross-stream event waits between the
+// ranks' threads, which a stream capture cannot hold.  The launches and
+// their order are the captured graph's.
+bool loop_comm(const gqmap_ctx *c) { return c->comm && c->comm->loop; }
 
 gqmap_status ensure_sub_graph(gqmap_ctx *c, int k) { return capture_steps(c, 1 << k, &c->sub[k]); }
 
@@ -2940,7 +3141,7 @@ gqmap_status ctx_set_images_device(gqmap_ctx *c, const double *dI1, const double
     GQ_HIP(pad_vv_device(dI2, Mo, No, d_scratch, c->stream));
     const size_t nvv = (size_t)(Mo + 2) * (No + 2);
     bool vv32 = c->fp32;
-    if (!vv32 && g_pol.vv_float)
+    if (!vv32 && c->pol.vv_float)
         GQ_HIP(f32_exact_device(d_scratch, nvv, d_flag, &vv32, c->stream));
     gqmap_status s = prepare_images(c, Mo, No, vv32);
     if (s != GQMAP_OK) return s;
@@ -3169,7 +3370,7 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
     // from rgb2gray are integers; their cubic padding stays in [-510, 765]):
     // same values, half the gather bytes.
     bool vv32 = c->fp32;
-    if (!vv32 && g_pol.vv_float) {
+    if (!vv32 && c->pol.vv_float) {
         vv32 = true;
         for (double v : VV)
             if ((double)(vvs_t)v != v) { vv32 = false; break; }
@@ -3364,9 +3565,9 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
              c->n_tiles);
     GQ_CHECK(n_iter >= 0, GQMAP_ERR_INVALID_ARG, "n_iter < 0");
     DeviceGuard dg(c->device);
-    if (c->comm && c->L == 1) (void)ensure_snap(c);  // deferred RCCL sequences (outside any capture)
+    gqmap_status s = comm_snap(c);  // deferred RCCL sequences (outside any capture)
+    if (s != GQMAP_OK) return s;
     Ctl h0;
-    gqmap_status s = GQMAP_OK;
     if (c->ctl_known) h0.it = c->ctl_it;
     else if ((s = read_ctl(c, &h0)) != GQMAP_OK) return s;
     int total = 0;
@@ -3375,7 +3576,7 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
         const int chunk = std::min(n_iter - total, TRACE_CAP);
         int left = chunk;
         c->ctl_known = false;
-        if (g_pol.graph) {
+        if (c->pol.graph && !loop_comm(c)) {
             // GRAPH_CHUNK-iteration graphs, then the remainder as graphs of
             // 2^k iterations (a short run replays graphs too)
             if (left >= GRAPH_CHUNK && (s = ensure_graph(c)) != GQMAP_OK) return s;
@@ -3445,19 +3646,20 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
              c->n_tiles);
     GQ_CHECK(n_iter >= 1, GQMAP_ERR_INVALID_ARG, "n_iter < 1");
     DeviceGuard dg(c->device);
-    if (c->comm && c->L == 1) (void)ensure_snap(c);
+    gqmap_status s = comm_snap(c);
+    if (s != GQMAP_OK) return s;
     Ctl h0;
-    gqmap_status s = read_ctl(c, &h0);
+    s = read_ctl(c, &h0);
     if (s != GQMAP_OK) return s;
     std::vector<hipEvent_t> ev((size_t)2 * n_iter + 2);
     for (auto &e : ev) GQ_HIP(hipEventCreate(&e));
     GQ_HIP(hipEventRecord(ev[0], c->stream));
-    if (deferred(c)) {  // the production sequences, both k_iter launches of each iteration bracketed
+    if (deferred(c)) {  // the production sequences, each iteration's k_iter launch bracketed
         for (int i = 0; i < n_iter; i += GRAPH_CHUNK)
             if ((s = launch_seq_deferred(c, std::min(GRAPH_CHUNK, n_iter - i), &ev[2 + 2 * i])) != GQMAP_OK) return s;
     } else {
         for (int i = 0; i < n_iter; ++i) {
-            if (c->comm) {  // both k_iter launches (boundary, interior) of the iteration
+            if (c->comm) {  // the iteration's one k_iter launch over the strip
                 if ((s = launch_step_rccl(c, ev[2 + 2 * i], ev[3 + 2 * i])) != GQMAP_OK) return s;
                 continue;
             }
@@ -3501,6 +3703,7 @@ gqmap_status gqmap_prepare(gqmap_ctx *c)
              "tile %d/%d: attach RCCL (gqmap_tile_attach_rccl) or use gqmap_tile_group_run", c->tile,
              c->n_tiles);
     DeviceGuard dg(c->device);
+    if (loop_comm(c)) return comm_snap(c);
     gqmap_status s = ensure_graph(c);
     if (s != GQMAP_OK) return s;
     GQ_HIP(hipGraphUpload(c->graph, c->stream));
@@ -3753,6 +3956,26 @@ static gqmap_status attach_common(gqmap_ctx *c)
     return GQMAP_OK;
 }
 
+// The buffers of an RCCL tile (either communicator): the totals table, and
+// for L = 1 the deferred-totals sequence's rows, gathered rows and snapshot.
+// Allocated here, once, so that every rank runs the same collective
+// sequence: a rank that cannot allocate them fails the attach instead of
+// quietly taking the exact per-iteration step (whose collectives would not
+// match its peers' sequences).
+static gqmap_status attach_comm(gqmap_ctx *c)
+{
+    gqmap_status s = attach_common(c);
+    if (s != GQMAP_OK) return s;
+    if (c->L == 1) {  // deferred-totals sequences (launch_seq_deferred)
+        const size_t NP = NFIX + c->L;
+        GQ_HIP(hipMalloc((void **)&c->d_rows, sizeof(fix128) * NP * GRAPH_CHUNK));
+        GQ_HIP(hipMalloc((void **)&c->d_seqg, sizeof(fix128) * NP * GRAPH_CHUNK * c->n_tiles));
+        GQ_CHECK(ensure_snap(c), GQMAP_ERR_HIP, "tile %d: deferred-sequence snapshot (%zu bytes) not allocated",
+                 c->tile, (size_t)c->MNL * NPLANES * c->rsz);
+    }
+    return GQMAP_OK;
+}
+
 gqmap_status gqmap_comm_unique_id(uint8_t id[128])
 {
     clear_error();
@@ -3787,15 +4010,65 @@ gqmap_status gqmap_tile_attach_rccl(gqmap_ctx *c, const uint8_t id[128])
         return GQMAP_ERR_HIP;
     }
     c->comm = cm;
-    gqmap_status s = attach_common(c);
-    if (s != GQMAP_OK) return s;
-    if (c->L == 1) {  // deferred-totals sequences (launch_seq_deferred)
-        const size_t NP = NFIX + c->L;
-        GQ_HIP(hipMalloc((void **)&c->d_rows, sizeof(fix128) * NP * GRAPH_CHUNK));
-        GQ_HIP(hipMalloc((void **)&c->d_seqg, sizeof(fix128) * NP * GRAPH_CHUNK * c->n_tiles));
-        (void)ensure_snap(c);
-    }
-    return GQMAP_OK;
+    return attach_comm(c);
+}
+
+// Not in the public header (tests): the loopback transport of n tile
+// contexts in one process (LoopGroup) -- gqmap_debug_loop_create, then
+// gqmap_debug_tile_attach_loop for tiles 0..n-1 (each tile then run from its
+// own host thread, exactly as RCCL ranks), gqmap_debug_loop_destroy after
+// every tile context is destroyed.  Returns the group or null.
+void *gqmap_debug_loop_create(int n, int device)
+{
+    if (n < 1) return nullptr;
+    DeviceGuard dg(device);
+    LoopGroup *g = new LoopGroup();
+    g->n = n;
+    g->device = device;
+    g->post.resize(n);
+    g->ready.assign(n, nullptr);
+    g->done.assign(n, nullptr);
+    for (int i = 0; i < n; ++i)
+        if (hipEventCreateWithFlags(&g->ready[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->done[i], hipEventDisableTiming) != hipSuccess) {
+            for (hipEvent_t e : g->ready) if (e) (void)hipEventDestroy(e);
+            for (hipEvent_t e : g->done) if (e) (void)hipEventDestroy(e);
+            delete g;
+            return nullptr;
+        }
+    return g;
+}
+
+void gqmap_debug_loop_destroy(void *group)
+{
+    LoopGroup *g = (LoopGroup *)group;
+    if (!g) return;
+    DeviceGuard dg(g->device);
+    for (hipEvent_t e : g->ready) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->done) if (e) (void)hipEventDestroy(e);
+    delete g;
+}
+
+// The collectives the group has completed (each counted once).
+unsigned long long gqmap_debug_loop_calls(void *group) { return group ? ((LoopGroup *)group)->calls : 0; }
+
+gqmap_status gqmap_debug_tile_attach_loop(gqmap_ctx *c, void *group)
+{
+    clear_error();
+    LoopGroup *g = (LoopGroup *)group;
+    GQ_CHECK(c && g, GQMAP_ERR_INVALID_ARG, "null argument");
+    GQ_CHECK(c->have_images, GQMAP_ERR_STATE, "attach after gqmap_set_images");
+    GQ_CHECK(!c->comm && !c->in_group && !c->host_xfer, GQMAP_ERR_STATE, "tile already has a transport");
+    GQ_CHECK(g->n == c->n_tiles && c->device == g->device, GQMAP_ERR_INVALID_ARG,
+             "loop group of %d ranks on device %d, tile %d of %d on device %d", g->n, g->device, c->tile, c->n_tiles,
+             c->device);
+    DeviceGuard dg(c->device);
+    RcclComm *cm = new RcclComm();
+    cm->nranks = c->n_tiles;
+    cm->rank = c->tile;
+    cm->loop = g;
+    c->comm = cm;
+    return attach_comm(c);
 }
 
 gqmap_status gqmap_tile_attach_host(gqmap_ctx *c)
@@ -3969,7 +4242,7 @@ void gqmap_destroy(gqmap_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     drop_graph(c);
     if (c->comm) {
-        (void)rccl()->CommDestroy(c->comm->comm);
+        if (c->comm->comm) (void)rccl()->CommDestroy(c->comm->comm);
         delete c->comm;
     }
     for (void *p : {(void *)c->d_rows, (void *)c->d_seqg})
