@@ -359,7 +359,8 @@ def parity_gate(r, engine, steps, precision, split, seed):
                    "number of iterations; literal: the fp64 restatement of the MATLAB, which differs by a rounding "
                    "or two per operation -- the solver's transient is chaotic, so that difference grows with the "
                    "iteration count (DESIGN.md 2; divergence: the same growth between the restatement and itself "
-                   "under a 1e-13 perturbation); literal_engine: the engine run in the reference's operation order")
+                   "under a 1e-13 perturbation); literal_engine: the engine run in the MATLAB source's expression "
+                   "order, non-fused IEEE (arith=literal)")
     return out
 
 
@@ -522,7 +523,7 @@ TRACK_ITS = 60  # iterations of the per-iteration divergence record (parity gate
 
 def literal_engine_leg(args, rank, opts, I1, I2, flo, unk, gate_its, device):
     """The literal-order engine (options arith="literal": every expression of
-    gqmap_gpu_mixture.m:87-182 in the reference's own order, k_iter_lit) on
+    gqmap_gpu_mixture.m:87-182 in MATLAB's expression order, non-fused IEEE, k_iter_lit) on
     the same pair, seed and steps: timed like the headline (settled clocks,
     gqmap_run graph replay), its k_iter_lit mean from an instrumented replay,
     and its flow after gate_its iterations for the parity gate (bit-identical
@@ -583,13 +584,71 @@ def run_c3(args, rank, world, local, barrier):
     elapsed = time.perf_counter() - t0
     px = sum(p.level(l)["I2"].size * its[l] for l in range(len(C3_SCALES)))
     a = aepe(flo, flow, unk)
+    top = p.level(len(C3_SCALES) - 1)
     p.close()
+    # the dominant (full-resolution) level's k_iter on its own: the same
+    # frames (the level's warped I1 and I2) and options in a single-level
+    # context, every launch bracketed by HIP events (gqmap_run_timed)
+    dom = None
+    if rank == 0:
+        from gqmap_opticalflow_amd import Engine
+        with Engine(opts, top["I1w"], top["I2"], "ctf", args.precision, device=local) as e:
+            e.init_state(seed=rank + len(C3_SCALES) - 1)
+            e.run_timed(min(args.steps, 20))
+            e.init_state(seed=rank + len(C3_SCALES) - 1)
+            done, total_ms, kernel_ms = e.run_timed(args.steps)
+            M, N = top["I2"].shape
+            dom = dict(level=f"{N}x{M}", its=done, kernel_avg_s=kernel_ms / max(done, 1) / 1e3, nodes=M * N,
+                       split=e.info().split)
     Mo, No = I1.shape
     return dict(elapsed=elapsed, pix_its=px, aepe=a, name=name, I1=I1, I2=I2, opts=dict(opts, engine="ctf"),
-                Mo=Mo, No=No, its=its,
+                Mo=Mo, No=No, its=its, flo=flo, unk=unk, seed=rank, dominant=dom,
                 workload=f"C3: {name} {No}x{Mo} coarse-to-fine, 5 levels 1/16..1 (30x40..480x640), "
                          f"gqmap_ctf K=11, {args.steps} its/level, device imresize/interp2/fillmissing; "
                          f"value counts sum over levels of level pixels x its")
+
+
+def parity_gate_c3(r, precision, its=12):
+    """The C3 pipeline's parity gate, after the timed region: the device
+    pyramid (5 levels, `its` iterations per level, the timed run's seed)
+    against the CPU pipeline (oracle.ctf_pipeline: the restated imresize /
+    interp2 / fillmissing plumbing around each level's solver) with the CPU
+    model of the kernel arithmetic (emul: bit-exact expected) and with the
+    literal fp64 restatement (literal: a rounding or two per operation,
+    DESIGN.md 2), from the same seeded per-level initial states
+    (tests/test_gpu_pyramid.py at 12 iterations per level)."""
+    from gqmap_opticalflow_amd import C3_SCALES, Pyramid, aepe, gauss_hermite, initial_state
+    from oracle import oracle
+    opts = dict(r["opts"], its=its)
+    opts.pop("engine", None)
+    seed = r["seed"]
+    hc = host_cpus()
+    t0 = time.perf_counter()
+    with Pyramid(opts, C3_SCALES, precision) as p:
+        p.set_images(r["I1"], r["I2"])
+        flow, lits, _ = p.run(seed=seed)
+    X, W = gauss_hermite(int(opts["K"]))
+
+    def init_fn(l, lo, M, N):
+        st = initial_state(lo, M, N, seed=seed + l, engine="ctf")
+        return oracle.State(st.muu, st.muv, st.sigu, st.sigv, st.pn, st.rou, st.w, st.alpha)
+
+    out = {"its_per_level": its, "levels": len(C3_SCALES), "aepe_gpu": aepe(r["flo"], flow, r["unk"])}
+    for solver in ("emu", "literal"):
+        t1 = time.perf_counter()
+        warp, _ = oracle.ctf_pipeline(opts, r["I1"], r["I2"], C3_SCALES, init_fn, solver=solver, X=X, W=W,
+                                      nthreads=hc["threads"], fp32=precision == "fp32")
+        k = "emul" if solver == "emu" else "literal"
+        out[f"aepe_cpu_{k}"] = aepe(r["flo"], warp, r["unk"])
+        out[f"aepe_delta_{k}"] = out["aepe_gpu"] - out[f"aepe_cpu_{k}"]
+        out[f"flow_bit_exact_{k}"] = bool(np.array_equal(flow, warp))
+        out[f"flow_max_abs_diff_{k}"] = float(np.max(np.abs(flow - warp)))
+        out[f"cpu_s_{k}"] = time.perf_counter() - t1
+    out["seconds"] = time.perf_counter() - t0
+    out["note"] = ("emul: CPU pipeline with the CPU model of the kernel arithmetic (gqmap_math.h) -- bit-exact; "
+                   "literal: the same pipeline with the fp64 restatement of legacy/gqmap_ctf.m, a rounding or two "
+                   "per operation away, amplified by the solver's chaotic transient (DESIGN.md 2)")
+    return out
 
 
 def run_c1(args, rank, world, local, barrier):
@@ -635,7 +694,10 @@ def run_c1(args, rank, world, local, barrier):
                                      "host<->device copies (PCIe-inclusive rate; not the value)"},
                 workload=f"C1: {name} {N}x{M} legacy/gqmap_cpu.m flow denoising (input = GT flow, unknowns 0), "
                          f"K=9, var=gama=1, dta=inf, {args.steps} its, sigma0 = U+2 (seed 0); flow resident in "
-                         f"HBM (gqmap_cpu_run_device); aepe = mean |mu - flow|")
+                         f"HBM (gqmap_cpu_run_device); aepe = mean |mu - flow|",
+                value_definition="device-resident (round 5 on): the flow already in HBM, results left there -- "
+                                 "not comparable with C1 values before round 5, which timed the host-array call; "
+                                 "compare kernel progress across rounds with host_arrays")
 
 
 def cpu_baseline_c1(flow, opts, budget_s: float = 8.0):
@@ -971,6 +1033,7 @@ def main():
                 out["clock_settle"]["cold_start_value"] = units / (cs * 1e-3 * args.steps) / 1e9
         if cfg == "c1":
             out["host_arrays"] = r["host_arrays"]
+            out["value_definition"] = r["value_definition"]
             # per pixel: node 2 x K x 6 flop, edges 4 x K^2 x ~40 flop (legacy/gqmap_cpu.m:20-54)
             fl = (2 * K * 6 + 4 * K * K * 40) * r["pixels"] * r["its"]
             out["roofline"] = {"bound": "valu", "achieved": fl / elapsed / 1e12, "peak": PEAK_TFLOPS["fp64"],
@@ -988,7 +1051,18 @@ def main():
                                "unit": "TFLOP/s", "frac": fl / secs / 1e12 / PEAK_TFLOPS[args.precision],
                                "traffic": traffic_per_launch(args.precision, cfg),
                                "kernel": "gq::k_iter<R,VT,2,Q> (all levels; timed by the pipeline wall clock)",
+                               "traffic_source": traffic_source(args.precision, cfg),
+                               "traffic_kernel": "the full-resolution level's k_iter (per launch)",
                                "algorithmic_bytes_per_node_iter": algorithmic_bytes_per_node("ctf", 1, Sb)}
+            dom = r.get("dominant")
+            if dom:
+                # the dominant level's kernel on its own, from HIP events
+                dl = roofline("ctf", 1, K, dom["nodes"], args.precision, dom["kernel_avg_s"], cfg,
+                              "gq::k_iter<R,VT,2,Q> (the full-resolution level)")
+                dl.update(level=dom["level"], its=dom["its"], split=dom["split"],
+                          kernel_timing="HIP events around every k_iter launch (gqmap_run_timed) of a single-level "
+                                        "context on the level's own frames (the pipeline's warped I1 and I2)")
+                out["roofline"]["dominant_level"] = dl
             out["config"]["its_per_level"] = r["its"]
         else:
             # tiled: the kernel mean over all pairs' launches; nodes = the
@@ -1062,6 +1136,15 @@ def main():
             for k in ("aepe_cpu_literal", "aepe_delta_literal"):
                 out[k] = par[k]
             out["colour_mismatch"] = par["colour_mismatch_literal"]
+        except Exception as e:
+            out["parity"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if rank == 0 and cfg == "c3" and not args.no_parity:
+        try:
+            par = parity_gate_c3(r, args.precision, args.parity_steps or 12)
+            out["parity"] = par
+            for k in ("aepe_cpu_emul", "aepe_cpu_literal", "aepe_delta_emul", "aepe_delta_literal",
+                      "flow_bit_exact_emul"):
+                out[k] = par[k]
         except Exception as e:
             out["parity"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and "map" in r and not args.no_parity:

@@ -314,15 +314,24 @@ gqmap_status gqmap_cpu_release(void)
 
 namespace {
 
-// Does p point into device memory of the current device (or managed memory)?
-bool on_device(const void *p)
+// Does p point into device memory of `device` (or managed memory)?  Memory
+// of another GPU would be read through peer access, or fault.
+bool on_device(const void *p, int device)
 {
     hipPointerAttribute_t at{};
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();  // a plain host pointer: clear the sticky error
         return false;
     }
-    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+    if (at.type == hipMemoryTypeManaged) return true;
+    return at.type == hipMemoryTypeDevice && at.device == device;
+}
+
+// Do the byte ranges [a, a + na) and [b, b + nb) overlap?
+bool overlap(const void *a, size_t na, const void *b, size_t nb)
+{
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return na && nb && x < y + nb && y < x + na;
 }
 
 // gqmap_cpu_run (DEV = false: host arrays, copied in and out) and
@@ -346,11 +355,24 @@ gqmap_status cpu_run(const gqmap_cpu_options *o, const double *flow, int M, int 
     DeviceGuard dg(device);
     const size_t MN = (size_t)M * N;
     if (DEV) {
-        GQ_CHECK(on_device(flow) && on_device(mu) && on_device(sigma) && on_device(rou) &&
-                     (!sigma0 || on_device(sigma0)) && (!trace || on_device(trace)),
-                 GQMAP_ERR_INVALID_ARG, "%s: every array must be device memory", fn);
-        GQ_CHECK(mu != flow && (const double *)sigma != sigma0, GQMAP_ERR_INVALID_ARG,
-                 "%s: mu must not alias flow, nor sigma sigma0", fn);
+        GQ_CHECK(on_device(flow, device) && on_device(mu, device) && on_device(sigma, device) &&
+                     on_device(rou, device) && (!sigma0 || on_device(sigma0, device)) &&
+                     (!trace || on_device(trace, device)),
+                 GQMAP_ERR_INVALID_ARG, "%s: every array must be device memory of device %d", fn, device);
+        // the outputs (written in place during the run) must not overlap each
+        // other or an input
+        const size_t b2 = sizeof(double) * 2 * MN;
+        const struct { const void *p; size_t n; } out[4] = {
+            {mu, b2}, {sigma, b2}, {rou, 2 * b2}, {trace, trace ? sizeof(double) * 3 * (size_t)o->its : 0}};
+        const struct { const void *p; size_t n; } in[2] = {{flow, b2}, {sigma0, sigma0 ? b2 : 0}};
+        for (int i = 0; i < 4; ++i) {
+            for (int j = i + 1; j < 4; ++j)
+                GQ_CHECK(!overlap(out[i].p, out[i].n, out[j].p, out[j].n), GQMAP_ERR_INVALID_ARG,
+                         "%s: output arrays %d and %d overlap (mu, sigma, rou, trace)", fn, i, j);
+            for (int j = 0; j < 2; ++j)
+                GQ_CHECK(!overlap(out[i].p, out[i].n, in[j].p, in[j].n), GQMAP_ERR_INVALID_ARG,
+                         "%s: output array %d (mu, sigma, rou, trace) overlaps %s", fn, i, j ? "sigma0" : "flow");
+        }
     }
     LgParams P{};
     P.M = M; P.N = N; P.K = o->K; P.its = o->its; P.min_its = o->min_its;

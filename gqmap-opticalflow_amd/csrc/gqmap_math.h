@@ -941,11 +941,44 @@ inline void lit_table_point(double *row8, double xi, double xj, double wi, doubl
 // Xq, Yq clamped to [1, N] x [1, M], the cell chosen by the reference's
 // if-chain, each tap weighted as (VV * ss) * tw, the taps added left to right
 // (first column parenthesised as the reference writes it), then /4.
+//
+// Execution forms of the literal loops (GQ_LIT_FORM; every form performs the
+// same IEEE operations on the same operands, so the bits never change --
+// tests/test_literal.py, tests/test_gpu_literal.py):
+//   0  round 5: the reference's if-chain as branches, `if a~=0` per point,
+//      every product of a point formed at the point;
+//   1  the cell chosen branch-free: after the clamp Xq is in [1, N], where
+//      the chain's 1 / floor(Xq) / N-1 is exactly min(floor(Xq), N-1) (the
+//      chain's first arm only sees Xq = 1 = floor(Xq)); `a~=0` is uniform
+//      over a gradient (alpha of one component, one guard flag), so the
+//      loop is versioned on it instead of testing it per point;
+//   2  as 1, and the column's products s*XI, t*XI formed once per meshgrid
+//      column (XI(r, c) = X(c) for every row r, gqmap_gpu_mixture.m:8): the
+//      same rounded products the per-point form computes.
+#ifndef GQ_LIT_FORM
+#define GQ_LIT_FORM 2
+#endif
+// the three changes separately (A/B): branch-free cell, versioned loop,
+// column products (default: those of GQ_LIT_FORM)
+#ifndef GQ_LIT_CELL
+#define GQ_LIT_CELL (GQ_LIT_FORM >= 1)
+#endif
+#ifndef GQ_LIT_HOIST
+#define GQ_LIT_HOIST (GQ_LIT_FORM >= 1)
+#endif
+#ifndef GQ_LIT_CSE
+#define GQ_LIT_CSE (GQ_LIT_FORM >= 2)
+#endif
 template <typename VP>
 GQ_HD double lit_interp(VP VV, int M2, int Mo, int No, double Xq, double Yq)
 {
     Xq = fmin(fmax(Xq, 1.0), (double)No);
     Yq = fmin(fmax(Yq, 1.0), (double)Mo);
+#if GQ_LIT_CELL
+    const double fx = fmin(floor(Xq), (double)(No - 1)), fy = fmin(floor(Yq), (double)(Mo - 1));
+    const int ix = (int)fx, iy = (int)fy;
+    const double so = Xq - fx, to = Yq - fy;
+#else
     int ix, iy;
     if (Xq <= 1.0) ix = 1;
     else if (Xq <= No - 1) ix = (int)floor(Xq);
@@ -954,6 +987,7 @@ GQ_HD double lit_interp(VP VV, int M2, int Mo, int No, double Xq, double Yq)
     else if (Yq <= Mo - 1) iy = (int)floor(Yq);
     else iy = Mo - 1;
     const double so = Xq - ix, to = Yq - iy;
+#endif
     const double t0 = ((2.0 - to) * to - 1.0) * to;
     const double t1 = (3.0 * to - 5.0) * to * to + 2.0;
     const double t2 = ((4.0 - 3.0 * to) * to + 1.0) * to;
@@ -1017,6 +1051,14 @@ struct LitAcc {
     }
 };
 
+// K of a K x K rule from K2 (uniform, a few scalar steps)
+GQ_HD int lit_k(int K2)
+{
+    int K = 1;
+    while (K * K < K2) ++K;
+    return K;
+}
+
 // Spectral coordinates shared by both gradients (:90-93, :120-123)
 struct LitCoef {
     double s, t, pr, sqrtpr, rsqrtpr;  // rsqrtpr = RN(1 / sqrtpr) (div_rcp)
@@ -1059,6 +1101,67 @@ GQ_HD Grad<double> lit_epi(const LitAcc &S, const LitCoef &c, double a, double o
     return g;
 }
 
+// The quadrature loop of a gradient, points k = r + K c in meshgrid order
+// (column c outer, row r inner: the reference's k = 1..K^2): pt(k, zi, zj)
+// returns the point's fval.  Form 2 forms s*XI and t*XI once per column.
+template <bool LIVE, typename TP, typename PT>
+GQ_HD void lit_points(TP tab, int K2, const LitCoef &c, double p, LitAcc &S, PT pt)
+{
+#if GQ_LIT_CSE
+    const int K = lit_k(K2);
+    for (int cc = 0, k = 0; cc < K; ++cc) {
+        const double XI = tab[tab_at(TL_XI, k)];
+        const double sXI = c.s * XI, tXI = c.t * XI;
+        for (int r = 0; r < K; ++r, ++k) {
+            const double XJ = tab[tab_at(TL_XJ, k)];
+            const double zi = sXI + c.t * XJ, zj = tXI + c.s * XJ;
+            S.add(tab, k, pt(k, zi, zj), zi, zj, p, c.sqrtpr, c.rsqrtpr, LIVE);
+        }
+    }
+#else
+    for (int k = 0; k < K2; ++k) {
+        const double XI = tab[tab_at(TL_XI, k)], XJ = tab[tab_at(TL_XJ, k)];
+        const double zi = c.s * XI + c.t * XJ, zj = c.t * XI + c.s * XJ;
+        S.add(tab, k, pt(k, zi, zj), zi, zj, p, c.sqrtpr, c.rsqrtpr, LIVE);
+    }
+#endif
+}
+
+template <typename TP, typename PT>
+GQ_HD void lit_points_dyn(TP tab, int K2, const LitCoef &c, double p, LitAcc &S, PT pt, bool live)
+{
+#if GQ_LIT_CSE
+    const int K = lit_k(K2);
+    for (int cc = 0, k = 0; cc < K; ++cc) {
+        const double XI = tab[tab_at(TL_XI, k)];
+        const double sXI = c.s * XI, tXI = c.t * XI;
+        for (int r = 0; r < K; ++r, ++k) {
+            const double XJ = tab[tab_at(TL_XJ, k)];
+            const double zi = sXI + c.t * XJ, zj = tXI + c.s * XJ;
+            S.add(tab, k, pt(k, zi, zj), zi, zj, p, c.sqrtpr, c.rsqrtpr, live);
+        }
+    }
+#else
+    for (int k = 0; k < K2; ++k) {
+        const double XI = tab[tab_at(TL_XI, k)], XJ = tab[tab_at(TL_XJ, k)];
+        const double zi = c.s * XI + c.t * XJ, zj = c.t * XI + c.s * XJ;
+        S.add(tab, k, pt(k, zi, zj), zi, zj, p, c.sqrtpr, c.rsqrtpr, live);
+    }
+#endif
+}
+
+template <typename TP, typename PT>
+GQ_HD void lit_loop(TP tab, int K2, const LitCoef &c, double p, bool live, LitAcc &S, PT pt)
+{
+#if GQ_LIT_HOIST
+    if (live) lit_points<true>(tab, K2, c, p, S, pt);
+    else lit_points<false>(tab, K2, c, p, S, pt);
+#else
+    // `live` tested at every point (LitAcc::add)
+    lit_points_dyn(tab, K2, c, p, S, pt, live);
+#endif
+}
+
 // node_grad_spectral with node_pot, (m, n) 0-based pixel of the frame
 template <typename TP, typename VP, typename IP>
 GQ_HD Grad<double> lit_node_grad(TP tab, int K2, VP VV, int M2, IP I1, int Mo, int No, double eps, double lamd,
@@ -1070,14 +1173,11 @@ GQ_HD Grad<double> lit_node_grad(TP tab, int K2, VP VV, int M2, IP I1, int Mo, i
     const double I = I1[m + (int64_t)Mo * n];
     const bool live = !guard || a != 0;
     LitAcc S;
-    for (int k = 0; k < K2; ++k) {
-        const double XI = tab[tab_at(TL_XI, k)], XJ = tab[tab_at(TL_XJ, k)];
-        const double zi = c.s * XI + c.t * XJ, zj = c.t * XI + c.s * XJ;
+    lit_loop(tab, K2, c, p, live, S, [&](int k, double zi, double zj) {
         const double x1 = so1 * zi + u1, x2 = so2 * zj + u2;
         const double d = I - lit_interp(VV, M2, Mo, No, (double)(n + 1) + x1, (double)(m + 1) + x2);
-        const double fval = tab[tab_at(TL_W, k)] * (-lamd * GQ_SQRT(eps + d * d));
-        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, c.rsqrtpr, live);
-    }
+        return tab[tab_at(TL_W, k)] * (-lamd * GQ_SQRT(eps + d * d));
+    });
     return lit_epi(S, c, a, o1, o2, p, T, true);
 }
 
@@ -1090,13 +1190,10 @@ GQ_HD Grad<double> lit_edge_grad(TP tab, int K2, double eps, double lams, bool g
     const double so1 = GQ_M_SQRT2 * o1, so2 = GQ_M_SQRT2 * o2;
     const bool live = !guard || a != 0;
     LitAcc S;
-    for (int k = 0; k < K2; ++k) {
-        const double XI = tab[tab_at(TL_XI, k)], XJ = tab[tab_at(TL_XJ, k)];
-        const double zi = c.s * XI + c.t * XJ, zj = c.t * XI + c.s * XJ;
+    lit_loop(tab, K2, c, p, live, S, [&](int k, double zi, double zj) {
         const double d = (so1 * zi + u1) - (so2 * zj + u2);
-        const double fval = tab[tab_at(TL_W, k)] * (-lams * GQ_SQRT(eps + d * d));
-        S.add(tab, k, fval, zi, zj, p, c.sqrtpr, c.rsqrtpr, live);
-    }
+        return tab[tab_at(TL_W, k)] * (-lams * GQ_SQRT(eps + d * d));
+    });
     return lit_epi(S, c, a, o1, o2, p, T, false);
 }
 

@@ -82,6 +82,8 @@ def gqmap_cpu_device(options: dict, flow, *, sigma0=None, seed: int = 0, return_
     _check_dev("flow", flow, (M, N, 2))
     if sigma0 is not None:
         _check_dev("sigma0", sigma0, (M, N, 2))
+        if sigma0.device != flow.device:
+            raise ValueError(f"sigma0 is on {sigma0.device}, flow on {flow.device}: one device")
     o = cpu_options(options)
     dev = flow.device
     mu, sigma, rou = _fortran_dev((M, N, 2), dev), _fortran_dev((M, N, 2), dev), _fortran_dev((M, N, 2, 2), dev)

@@ -60,8 +60,12 @@ typedef enum gqmap_precision { GQMAP_FP64 = 0, GQMAP_FP32 = 1 } gqmap_precision;
  *          folded into a scale) -- within a rounding or two per gradient of
  *          the reference's expressions, the fastest form.
  *  LITERAL every expression of node_grad_spectral / edge_grad_spectral /
- *          node_pot / edge_pot (gqmap_gpu_mixture.m:87-182) in the
- *          reference's own order, no fused operations: bit-identical to the
+ *          node_pot / edge_pot (gqmap_gpu_mixture.m:87-182) in MATLAB's
+ *          expression order under non-fused IEEE semantics (left to right,
+ *          every operation correctly rounded).  That is how the .m source
+ *          reads; the reference itself ran arrayfun JIT-compiled for the
+ *          GPU, which may contract to FMA, so this is a restatement of the
+ *          source's order, not a replay of what MATLAB executed.  Bit-identical to the
  *          literal restatement oracle/gqmap_oracle.c while the alpha update
  *          is off (L = 1, or it <= alpha_start).  fp64 mixture engine only,
  *          one lane per node (split 0 or 1). */

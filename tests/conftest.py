@@ -21,11 +21,13 @@ def oracle_lib():
 
 @pytest.fixture(scope="session", autouse=True)
 def _torch_hip_runtime_first(request):
-    """GPU runs: PyTorch bundles its own HIP/HSA runtime beside the /opt/rocm
-    one libgqmap.so links; in one process the two coexist only when torch's
-    initialises first (the other order leaves torch with "No HIP GPUs are
-    available"), as in bench.py.  The device-array tests need torch tensors,
-    so torch.cuda is initialised before any test calls the library."""
+    """GPU runs: torch is loaded and torch.cuda initialised before any test
+    calls the library, as in bench.py.  Loaded after torch, libgqmap.so binds
+    to torch's bundled libamdhip64 / librccl (their SONAMEs match the names
+    the library asks for): one HIP runtime in the process
+    (tests/test_gpu_runtime.py).  In the other order two runtimes load and
+    torch reports "No HIP GPUs are available".  The device-array tests need
+    torch tensors."""
     if any(item.get_closest_marker("gpu") for item in request.session.items):
         import torch
         if torch.cuda.is_available():

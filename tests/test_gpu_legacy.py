@@ -107,6 +107,17 @@ def test_legacy_device_arrays_rejects_host_and_row_major():
     rc = load().gqmap_cpu_run_device(C.byref(o), flow.ctypes.data, 8, 9, None, C.c_uint64(0),
                                      *[a.ctypes.data for a in out], None, None, 0)
     assert rc != 0
+    # ... and outputs that overlap an input or each other (partial overlaps
+    # included), with every array on the device
+    n = 8 * 9 * 2
+    buf = torch.zeros(6 * n, dtype=torch.float64, device="cuda")
+    base = buf.data_ptr()
+    f_, mu_, sg_, rou_ = base, base + 8 * n, base + 16 * n, base + 24 * n
+    ok = load().gqmap_cpu_run_device(C.byref(o), f_, 8, 9, None, C.c_uint64(0), mu_, sg_, rou_, None, None, 0)
+    assert ok == 0, load().gqmap_last_error()
+    for args in ((f_, f_ + 8 * 8, sg_, rou_), (f_, mu_, mu_ + 8 * n - 8, rou_), (f_, mu_, sg_, sg_ + 8)):
+        rc = load().gqmap_cpu_run_device(C.byref(o), args[0], 8, 9, None, C.c_uint64(0), *args[1:], None, None, 0)
+        assert rc != 0 and b"overlap" in load().gqmap_last_error()
 
 
 @pytest.mark.parametrize("name", ["Hydrangea", "rubberwhale"])

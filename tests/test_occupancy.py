@@ -33,7 +33,19 @@ LIMITS = {
     # profiles/r05_node_pair_ab.txt) and the strong-scaling strips (mixture Q=2)
     "_ZN2gq6k_iterIddLi2ELi4ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
     "_ZN2gq6k_iterIdfLi0ELi2ELb0EEEvNS_10IterParamsIT_T0_EE": 256,
+    # the literal-order engine on integer frames (arith = literal, C2's
+    # parity-carrying arithmetic), plain and non-temporal stores: 3 waves
+    "_ZN2gq10k_iter_litIfLb0EEEvNS_10IterParamsIdT_EE": 168,
+    "_ZN2gq10k_iter_litIfLb1EEEvNS_10IterParamsIdT_EE": 168,
 }
+# kernels that must run without a private (scratch) segment: the C2 kernels
+# of both arithmetics (round 5's literal kernel carried 20 bytes of it)
+NO_SCRATCH = (
+    "_ZN2gq6k_iterIdfLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
+    "_ZN2gq6k_iterIffLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
+    "_ZN2gq10k_iter_litIfLb0EEEvNS_10IterParamsIdT_EE",
+    "_ZN2gq10k_iter_litIfLb1EEEvNS_10IterParamsIdT_EE",
+)
 
 
 def _kernel_registers(tmp):
@@ -50,8 +62,9 @@ def _kernel_registers(tmp):
         name = re.search(r"\n\s*\.name:\s+(\S+)", "\n" + block)
         v = re.search(r"\.vgpr_count:\s+(\d+)", block)
         a = re.search(r"\.agpr_count:\s+(\d+)", block)
+        sc = re.search(r"\.private_segment_fixed_size:\s+(\d+)", block)
         if name and v:
-            regs[name.group(1)] = (int(v.group(1)), int(a.group(1)) if a else 0)
+            regs[name.group(1)] = (int(v.group(1)), int(a.group(1)) if a else 0, int(sc.group(1)) if sc else 0)
     return regs
 
 
@@ -61,5 +74,7 @@ def test_headline_kernels_keep_their_waves(tmp_path):
     regs = _kernel_registers(str(tmp_path))
     for name, limit in LIMITS.items():
         assert name in regs, name
-        v, a = regs[name]
+        v, a, _ = regs[name]
         assert v <= limit and a == 0, f"{name}: {v} VGPRs + {a} AGPRs > {limit}"
+    for name in NO_SCRATCH:
+        assert regs[name][2] == 0, f"{name}: {regs[name][2]} bytes of scratch"
