@@ -353,7 +353,10 @@ __device__ __forceinline__ void acc_add_agent(unsigned long long *acc4, fix128 v
 }
 // The last workgroup: Ctl::acc -> tot[] (LDS), then clear acc for the next
 // iteration.  All 256 threads call it.
-__device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long long *sh)
+// acc_src: the accumulators to reduce (default Ctl::acc; the dataflow
+// kernel's per-iteration slots, k_iter_flow).
+__device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long long *sh,
+                               unsigned long long *acc_src = nullptr)
 {
     const int NPR = F.L > 1 ? NFIX + F.L : NFIX;
     const int tid = threadIdx.x;
@@ -361,7 +364,7 @@ __device__ void fin_reduce_acc(const FinParams &F, double *tot, unsigned long lo
     if (tid < 4 * NPR) {
         // all slices' loads in flight together, then the clears (one memory
         // round trip instead of eight: finalize 2.9 -> ~1 us)
-        unsigned long long *a = &F.ctl->acc[0][0][0] + tid;
+        unsigned long long *a = (acc_src ? acc_src : &F.ctl->acc[0][0][0]) + tid;
         unsigned long long v[ACC_SLICES];
 #pragma unroll
         for (int x = 0; x < ACC_SLICES; ++x) v[x] = __hip_atomic_load(a + x * SL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -825,7 +828,7 @@ template <typename R, typename VT, int ENG, int Q, bool EDGE_FIRST, bool COH = f
           bool LIT = false>
 __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, int it, int parity,
                                           int part_r, TileLdsQ<R, Q> &lds, int l0, int l1, double Tcur,
-                                          bool tab_ready)
+                                          bool tab_ready, unsigned long long *acc_ring = nullptr)
 {
     static_assert(!LIT || (ENG == 0 && Q == 1 && sizeof(R) == 8), "literal order: fp64 mixture, Q = 1");
     constexpr bool RS = Q == 0;                       // role split (node / edge waves)
@@ -1055,7 +1058,9 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
         const int lq = tid - NFIX;  // dalpha of the components this block ran
         if (tid < NFIX || (P.L > 1 && lq >= l0 && lq < l1))
             v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        if (P.fused || P.tile_acc) {
+        if (acc_ring) {  // the dataflow kernel's slot of this iteration (k_iter_flow)
+            if (v != 0) acc_add_agent(acc_ring + ((blockIdx.x % ACC_SLICES) * (NFIX + GQMAP_LMAX) + tid) * 4, v);
+        } else if (P.fused || P.tile_acc) {
             if (v != 0) acc_add_agent(&ctl->acc[blockIdx.x % ACC_SLICES][tid][0], v);
         } else {
             store_part_agent(P.partials, P.fin.nblocks, part_r, tid, v);
@@ -1545,6 +1550,224 @@ __global__ __launch_bounds__(256) void k_persist_snap(const Ctl *ctl, const unsi
     }
 }
 
+// ---------------------------------------------------------------------------
+// Dataflow launch of the single-scale engine (policy `flow`, opt-in; fp64/fp32
+// mixture, L = 1, one lane per node, whole grid).  One launch runs a chunk of
+// iterations without a grid barrier: resident workgroups claim (iteration,
+// tile) items in order from the queue of their XCD (blockIdx & 7; each XCD's
+// queue walks its band of tiles, iteration-major) and run one tile of one
+// iteration each -- iter_tile, the same arithmetic and bits as k_iter.  Item
+// (j, t) starts when tile t and its four neighbours have finished iteration
+// j - 1 (Jacobi: it reads their state j - 1; and the buffer it writes held
+// state j - 2, which they read during j - 1), and when iterations up to j - 2
+// are finalized.  So the tiles of iteration j + 1 fill the CUs that the tail
+// of iteration j leaves idle: a launch per iteration pays for its busiest
+// CU's tile count (C2: 925 tiles on 768 resident slots).
+//
+// Deadlock-free without co-residency: an item is claimed only by a running
+// workgroup, which holds it until done, and waits only for items earlier in
+// its own queue's order or of the previous iteration in a neighbouring band;
+// the earliest unfinished item therefore always has its inputs.  Spins are
+// still bounded: a timeout raises the persistent path's failure word
+// (BAR_FAIL), every workgroup leaves, and the host restores the chunk's
+// snapshot and goes on with one launch per iteration (persist_recover).
+//
+// Totals: each tile adds its exact sums into the accumulator slot of its
+// iteration (j & 1); the tile arriving last for iteration j waits for
+// finalize(j - 1), then reduces the slot and runs fin_apply (acquire and
+// release fences around it: the previous finalizer may have run on another
+// XCD) and publishes the finalized count.  The stop rule: finalize(s) stores
+// 1 + s in the stop word before it publishes; items of iteration >= s + 2
+// see it (they wait for finalize(s)) and leave; iteration s + 1 may already
+// have run -- it wrote the buffer of state s - 1 -- and its finalize is
+// skipped, so Ctl and the buffer holding state s stay as the whole-grid run
+// leaves them.  State moves between workgroups through device-coherent
+// (agent-scope) loads and stores (ld_state / st_state).
+// ---------------------------------------------------------------------------
+constexpr int FL_LINE = 32;                        // 32-bit words per 128-byte line
+constexpr int FL_Q = 0;                            // 8 per-XCD claim counters, a line each
+constexpr int FL_FIN = 8 * FL_LINE;                // iterations finalized (launch-local)
+constexpr int FL_STOP = 9 * FL_LINE;               // 1 + the launch-local iteration that stopped the run
+constexpr int FL_EXIT = 10 * FL_LINE;              // workgroups that have left
+constexpr int FL_ARR = 11 * FL_LINE;               // arrival tickets of slots 0, 1 (a line each)
+constexpr int FL_ACC = 13 * FL_LINE;               // 2 slots of ACC_SLICES x (NFIX + LMAX) x 4 u64 limbs
+constexpr int FL_ACC_SLOT = ACC_SLICES * (NFIX + GQMAP_LMAX) * 4;  // u64 per slot
+constexpr int FL_DONE = FL_ACC + 2 * 2 * FL_ACC_SLOT;              // per tile: iterations done (launch-local)
+constexpr int flow_words(int ntiles) { return FL_DONE + ntiles; }
+
+// Wait (wave 0 polls, the workgroup follows) until item (j, tile) may run.
+// Returns 1: run it; 0: leave (the run stopped before iteration j - 1, or a
+// failure -- injected, another workgroup's, or this spin's own timeout).
+__device__ __forceinline__ int flow_wait(unsigned *fl, unsigned *bar, int tiles_m, int ntiles, int tile, int j,
+                                         int *sh)
+{
+    if (threadIdx.x < 64) {
+        const int x = threadIdx.x;
+        const int tm = tile % tiles_m;
+        int dep = -1;  // the tile whose iteration j - 1 this lane waits for
+        if (j > 0) {
+            if (x == 0) dep = tile;
+            else if (x == 1 && tm > 0) dep = tile - 1;
+            else if (x == 2 && tm < tiles_m - 1 && tile + 1 < ntiles) dep = tile + 1;
+            else if (x == 3 && tile >= tiles_m) dep = tile - tiles_m;
+            else if (x == 4 && tile + tiles_m < ntiles) dep = tile + tiles_m;
+        }
+        unsigned spins = 0;
+        int go = 1;
+        while (true) {
+            bool ok = true, leave = false;
+            if (dep >= 0) ok = __hip_atomic_load(fl + FL_DONE + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)j;
+            else if (x == 5 && j >= 2) ok = __hip_atomic_load(fl + FL_FIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)(j - 1);
+            else if (x == 6) {
+                const unsigned st = __hip_atomic_load(fl + FL_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                leave = st != 0 && (int)st - 1 <= j - 2;
+            } else if (x == 7) {
+                leave = __hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            } else if (x == 8) {  // injected failure (tests): at the first item of iteration j
+                leave = __hip_atomic_load(bar + BAR_INJECT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(j + 1);
+                if (leave) __hip_atomic_store(bar + BAR_FAIL, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (__any(leave)) { go = 0; break; }
+            if (__all(ok)) break;
+            if (++spins > BAR_SPIN_LIMIT) {
+                if (x == 0) __hip_atomic_store(bar + BAR_FAIL, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                go = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(GQ_PERSIST_SLEEP);
+        }
+        if (x == 0) *sh = go;
+    }
+    __syncthreads();
+    return *sh;
+}
+
+// The last tile of iteration j to arrive: finalize(j) after finalize(j - 1).
+__device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, unsigned long long *slot, int j,
+                              double *tot, unsigned long long *sh, int *shf)
+{
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        int go = 1;
+        while (__hip_atomic_load(fl + FL_FIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)j) {
+            if (__hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+                ++spins > BAR_SPIN_LIMIT) {
+                __hip_atomic_store(bar + BAR_FAIL, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                go = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(GQ_PERSIST_SLEEP);
+        }
+        // a run stopped at an earlier iteration: Ctl keeps that iteration
+        if (go && __hip_atomic_load(fl + FL_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) go = 2;
+        *shf = go;
+    }
+    __syncthreads();
+    const int go = *shf;
+    if (go == 0) return;
+    if (go == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // Ctl and the trace as the previous finalizer left them
+        fin_reduce_acc(F, tot, sh, slot);
+        if (threadIdx.x == 0) {
+            fin_apply(F, tot);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (F.ctl->stop) __hip_atomic_store(fl + FL_STOP, (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(fl + FL_ARR + (j & 1) * FL_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fl + FL_FIN, (unsigned)(j + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// snap: Ctl as the launch found it (k_persist_snap, launched just before):
+// a workgroup dispatched late must not read Ctl after a finalize changed it.
+#ifndef GQ_FLOW_WAVES  // waves per SIMD the allocation must allow (3: <= 168 VGPRs, as k_iter on C2)
+#define GQ_FLOW_WAVES 3
+#endif
+#ifndef GQ_FLOW_MIX  // node-first / edge-first alternation among co-resident workgroups
+#define GQ_FLOW_MIX 0
+#endif
+#ifndef GQ_FLOW_COH  // device-coherent state access (0: plain -- timing experiments only, not coherent)
+#define GQ_FLOW_COH 1
+#endif
+#ifndef GQ_FLOW_PREFETCH  // claim the next item while the current one runs
+#define GQ_FLOW_PREFETCH 1
+#endif
+template <typename R, typename VT>
+__global__ __launch_bounds__(BLOCK, GQ_FLOW_WAVES) void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles,
+                                                        const Ctl *snap)
+{
+    unsigned *bar = P.bar;
+    // a stopped run, or a failed launch earlier in the replay (whose
+    // snapshot the host restores): nothing to do but take the exit ticket
+    const bool run = !snap->stop &&
+                     __hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    const int it0 = snap->it, done0 = snap->done;
+    const double T0 = snap->T;
+    const int b = blockIdx.x, xcd = b & 7;
+    int s0 = 0;
+    for (int y = 0; y < xcd; ++y) s0 += (ntiles - y + 7) >> 3;
+    const int nb = (ntiles - xcd + 7) >> 3;  // this XCD's band: tiles [s0, s0 + nb)
+    const bool edge_first = GQ_FLOW_MIX && ((((b >> 3) / P.cu_slots) & 1) != GQ_PHASE_MIX_OTHER_INV);
+    __shared__ TileLdsQ<R, 1> lds;
+    __shared__ int sh_i, sh_go, sh_last;
+    __shared__ double tot[NFIX + GQMAP_LMAX];
+    __shared__ unsigned long long sh_acc[4 * (NFIX + GQMAP_LMAX)];
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(fl + FL_ACC);
+    unsigned *q = fl + FL_Q + xcd * FL_LINE;
+    unsigned nxt = 0;  // thread 0: the claim issued during the previous item
+    if (run && nb > 0 && GQ_FLOW_PREFETCH && threadIdx.x == 0)
+        nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (run && nb > 0) {
+        if (threadIdx.x == 0) {
+            if (GQ_FLOW_PREFETCH) {
+                sh_i = (int)nxt;
+                // the next claim goes out now; its latency hides behind this
+                // item's first state loads (a claim past the last item is harmless)
+                if ((int)nxt / nb < n_iter) nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                sh_i = (int)__hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        const int i = sh_i, j = i / nb;
+        if (j >= n_iter) break;
+        const int tile = s0 + i % nb;
+        if (!flow_wait(fl, bar, P.tiles_m, ntiles, tile, j, &sh_go)) break;
+        const int it = it0 + j, parity = (done0 + j) & 1;
+        double T = T0;  // fin_apply's temperature decay after each earlier iteration
+        if (P.fin.t_decay_every > 0)
+            for (int q = it0; q < it; ++q)
+                if (q % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
+        unsigned long long *slot = acc + (size_t)(j & 1) * FL_ACC_SLOT;
+        if (GQ_FLOW_MIX && edge_first)
+            iter_tile<R, VT, 0, 1, true, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
+        else
+            iter_tile<R, VT, 0, 1, false, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
+        // publish: every wave's stores (state, rou, the slot's sums) are done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(fl + FL_DONE + tile, (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh_last = __hip_atomic_fetch_add(fl + FL_ARR + (j & 1) * FL_LINE, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ntiles - 1);
+        }
+        __syncthreads();
+        if (sh_last) flow_finalize(P.fin, fl, bar, slot, j, tot, sh_acc, &sh_go);
+        __syncthreads();
+    }
+    // the last workgroup out clears the queue state for the next launch
+    __syncthreads();
+    if (threadIdx.x == 0)
+        sh_last = __hip_atomic_fetch_add(fl + FL_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (sh_last) {
+        for (int w = threadIdx.x; w < flow_words(ntiles); w += blockDim.x)
+            __hip_atomic_store(fl + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_finalize(FinParams F)
 {
     if (F.ctl->stop) return;
@@ -1852,6 +2075,7 @@ struct Policy {
     int persist = 1;       // persistent launch of the small ctf levels
     int persist_cap = -1;  // resident workgroups assumed by the persistent launch (-1: occupancy query)
     int graph = 1;         // replayed hipGraphs (0: direct launches)
+    int flow = 0;          // dataflow launch of the single-scale engine (k_iter_flow; opt-in)
     int vv_float = 1;      // float padded-frame store when exact
     int verbose = 0;       // recovery messages on stderr
 };
@@ -1925,6 +2149,8 @@ struct gqmap_ctx {
     fix128 *seq_row = nullptr;  // the row of the iteration being issued
     bool spec_now = false;      // the launches being issued run by Ctl::it_i / done_i / T_i
     gq::Policy pol = gq::g_pol;  // execution policies, fixed at creation
+    unsigned *d_flow = nullptr;  // k_iter_flow queue state (flow_words(tiles) words, zero between launches)
+    int flow_n = 0;
 };
 
 
@@ -2883,11 +3109,14 @@ gqmap_status launch_step(gqmap_ctx *c)
     return launch_tail(c);
 }
 
-// n iterations: one persistent launch for small ctf grids, else n steps
+bool launch_flow(gqmap_ctx *c, int n, bool dry = false);
+
+// n iterations: one persistent launch for small ctf grids (or one dataflow
+// launch, policy flow), else n steps
 gqmap_status launch_steps(gqmap_ctx *c, int n)
 {
     c->ctl_known = false;
-    if (launch_persist(c, n)) return GQMAP_OK;
+    if (launch_persist(c, n) || launch_flow(c, n)) return GQMAP_OK;
     gqmap_status st = GQMAP_OK;
     if (deferred(c)) {
         for (int i = 0; i < n && st == GQMAP_OK; i += GRAPH_CHUNK) st = launch_seq_deferred(c, std::min(GRAPH_CHUNK, n - i));
@@ -2898,6 +3127,58 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
 }
 
 void drop_graph(gqmap_ctx *c);
+
+// ---- dataflow launch (k_iter_flow, policy flow) ---------------------------
+template <typename R, typename VT>
+bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
+{
+    const int ntiles = c->tiles_m * c->tiles_n;
+    if (c->flow_n != flow_words(ntiles)) {  // (re)allocate outside any capture
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(c->stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+        if (c->d_flow) (void)hipFree(c->d_flow);
+        c->d_flow = nullptr;
+        c->flow_n = 0;
+        if (hipMalloc((void **)&c->d_flow, sizeof(unsigned) * flow_words(ntiles)) != hipSuccess) {
+            c->d_flow = nullptr;
+            return false;
+        }
+        if (hipMemsetAsync(c->d_flow, 0, sizeof(unsigned) * flow_words(ntiles), c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return false;
+        c->flow_n = flow_words(ntiles);
+    }
+    if (!ensure_snap(c)) return false;
+    if (dry) return true;
+    {
+        const int64_t nv = (int64_t)c->MNL * NPLANES;
+        const int grid = (int)std::min<int64_t>((nv + 255) / 256, 512);
+        k_persist_snap<R><<<grid, 256, 0, c->stream>>>(c->d_ctl, c->d_bar, (const R *)c->d_st[0],
+                                                       (const R *)c->d_st[1], (R *)c->d_snap, c->d_snap_ctl, nv);
+    }
+    IterParams<R, VT> P = iter_params<R, VT>(c);
+    static const int2 shape = kernel_shape(k_iter_flow<R, VT>);
+    P.cu_group = 1;
+    P.cu_slots = std::max(1, shape.y / 8);
+    // one workgroup per resident slot (more would only queue behind them)
+    const int G = std::max(8, std::min(shape.x * shape.y, ntiles));
+    k_iter_flow<R, VT><<<G, BLOCK, 0, c->stream>>>(P, n, c->d_flow, ntiles, c->d_snap_ctl);
+    return true;
+}
+
+// n iterations as one k_iter_flow launch when the policy asks for it and the
+// context qualifies (single-scale mixture, L = 1, one lane per node, the
+// whole grid, fast arithmetic); dry: only the check (and the buffers).
+bool launch_flow(gqmap_ctx *c, int n, bool dry)
+{
+    if (!c->pol.flow || c->persist_off || c->opt.engine != GQMAP_ENGINE_MIXTURE || c->L != 1 || c->n_tiles != 1 ||
+        c->comm || c->nranks != 0 || !fused_finalize(c) || c->kq != 1 || c->lit || n < 1)
+        return false;
+    if (c->fp32) return launch_flow_t<float, float>(c, n, dry);
+    if (c->vv32) return launch_flow_t<double, vvs_t>(c, n, dry);
+    return launch_flow_t<double, double>(c, n, dry);
+}
 
 // A persistent launch whose grid barrier gave up (workgroups not all
 // resident -- another process or stream holding CUs -- or descheduled past
@@ -2924,6 +3205,7 @@ gqmap_status persist_recover(gqmap_ctx *c, bool *recovered)
     GQ_HIP(hipMemcpyAsync(c->d_st[h.done & 1], c->d_snap, c->snap_bytes, hipMemcpyDeviceToDevice, c->stream));
     GQ_HIP(hipMemcpyAsync(c->d_ctl, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToDevice, c->stream));
     GQ_HIP(hipMemsetAsync(c->d_bar, 0, sizeof(unsigned) * BAR_WORDS, c->stream));
+    if (c->d_flow) GQ_HIP(hipMemsetAsync(c->d_flow, 0, sizeof(unsigned) * c->flow_n, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
     if (c->pol.verbose)
         fprintf(stderr, "gqmap: persistent launch failed (%d workgroups); restored iteration %d, "
@@ -3004,6 +3286,7 @@ gqmap_status capture_steps(gqmap_ctx *c, int n, hipGraphExec_t *out)
 {
     if (*out) return GQMAP_OK;
     (void)launch_persist(c, n, true);  // occupancy query, snapshot buffers: outside the capture
+    (void)launch_flow(c, n, true);
     gqmap_status st0 = comm_snap(c);  // the deferred RCCL sequence's snapshot
     if (st0 != GQMAP_OK) return st0;
     hipGraph_t g;
@@ -3588,7 +3871,7 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
             // the remainder as ONE launch / one sequence, directly: as 2^k
             // graphs it would pay a snapshot and a grid-barrier start-up, or
             // a snapshot, an all-gather and a finalize, per sub-graph)
-            const bool one = left > 0 && (deferred(c) || launch_persist(c, left, true));
+            const bool one = left > 0 && (deferred(c) || launch_persist(c, left, true) || launch_flow(c, left, true));
             if (!one) {
                 for (int k = SUB_GRAPHS - 1; k >= 0; --k)
                     if (left & (1 << k)) {
@@ -3654,9 +3937,17 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     std::vector<hipEvent_t> ev((size_t)2 * n_iter + 2);
     for (auto &e : ev) GQ_HIP(hipEventCreate(&e));
     GQ_HIP(hipEventRecord(ev[0], c->stream));
+    int timed = n_iter;  // event pairs summed into iter_kernel_ms
     if (deferred(c)) {  // the production sequences, each iteration's k_iter launch bracketed
         for (int i = 0; i < n_iter; i += GRAPH_CHUNK)
             if ((s = launch_seq_deferred(c, std::min(GRAPH_CHUNK, n_iter - i), &ev[2 + 2 * i])) != GQMAP_OK) return s;
+    } else if (launch_flow(c, n_iter, true)) {  // one pair around each chunk's dataflow launch
+        timed = 0;
+        for (int i = 0; i < n_iter; i += GRAPH_CHUNK, ++timed) {
+            GQ_HIP(hipEventRecord(ev[2 + 2 * timed], c->stream));
+            (void)launch_flow(c, std::min(GRAPH_CHUNK, n_iter - i));
+            GQ_HIP(hipEventRecord(ev[3 + 2 * timed], c->stream));
+        }
     } else {
         for (int i = 0; i < n_iter; ++i) {
             if (c->comm) {  // the iteration's one k_iter launch over the strip
@@ -3675,7 +3966,7 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     float t = 0;
     GQ_HIP(hipEventElapsedTime(&t, ev[0], ev[1]));
     double sum = 0;
-    for (int i = 0; i < n_iter; ++i) {
+    for (int i = 0; i < timed; ++i) {
         float k = 0;
         GQ_HIP(hipEventElapsedTime(&k, ev[2 + 2 * i], ev[3 + 2 * i]));
         sum += k;
@@ -3687,6 +3978,18 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
         bool again = false;
         if ((s = deferred_recover(c, h, &again)) != GQMAP_OK) return s;
         if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+    }
+    if (c->d_snap && !c->comm) {  // a failed persistent / dataflow launch: restored, finished per launch
+        bool rec = false;
+        if ((s = persist_recover(c, &rec)) != GQMAP_OK) return s;
+        if (rec) {
+            if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+            for (int i = h.it - h0.it; i < n_iter && !h.stop; ++i) {
+                launch_iter(c);
+                if ((s = launch_tail(c)) != GQMAP_OK) return s;
+                if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
+            }
+        }
     }
     if (n_done) *n_done = h.it - h0.it;
     if (total_ms) *total_ms = t;
@@ -3769,7 +4072,7 @@ int gqmap_debug_policy(const char *name, int value)
         {"lpar_xcd", &g_pol.lpar_xcd, 1},    {"fused_finalize", &g_pol.fused_finalize, 1},
         {"persist", &g_pol.persist, 1},      {"persist_cap", &g_pol.persist_cap, -1},
         {"graph", &g_pol.graph, 1},          {"vv_float", &g_pol.vv_float, 1},
-        {"verbose", &g_pol.verbose, 0},
+        {"verbose", &g_pol.verbose, 0},      {"flow", &g_pol.flow, 0},
     };
     for (const Field &f : fields)
         if (std::strcmp(f.n, name) == 0) {
@@ -4251,7 +4554,7 @@ void gqmap_destroy(gqmap_ctx *c)
     for (void *p : c->d_halo)
         if (p) (void)hipFree(p);
     void *bufs[] = {c->d_VV, c->d_I1, c->d_st[0], c->d_st[1], c->d_tab, c->d_ctl, (void *)c->d_partials, c->d_trace,
-                    c->d_truth, (void *)c->d_bar, c->d_snap, (void *)c->d_snap_ctl};
+                    c->d_truth, (void *)c->d_bar, c->d_snap, (void *)c->d_snap_ctl, (void *)c->d_flow};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
     for (void *p : {(void *)c->h_ctl, (void *)c->h_ring, (void *)c->h_fail})

@@ -1,0 +1,119 @@
+"""The dataflow launch of the single-scale engine (policy flow, k_iter_flow):
+resident workgroups claim (iteration, tile) items from per-XCD queues and
+start a tile's next iteration as soon as it and its four neighbours have
+finished the previous one (gqmap_gpu_mixture.m:29-46 is a Jacobi update), a
+chunk of up to 50 iterations per launch.  An execution form only: the
+arithmetic is k_iter's iter_tile, so the trace and state must be the
+per-launch path's bit for bit -- over graph chunks and leftovers, with the
+stop rule firing anywhere in a chunk, and after a failed launch (restored
+from its snapshot, finished with one launch per iteration)."""
+import numpy as np
+import pytest
+
+from tests import _golden as G
+from tests.test_gpu_parity import _policy
+
+pytestmark = pytest.mark.gpu
+
+
+def _c2(its_tor=None):
+    from gqmap_opticalflow_amd import flow_to_color, flowio
+    I1, I2, gt = flowio.load_pair("rubberwhale")
+    _, _, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
+    o = dict(K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdad=1.0, lambdas=5.0,
+             minu=minu, maxu=maxu, minv=minv, maxv=maxv)
+    return I1, I2, o
+
+
+def _run(o, I1, I2, its, flow, precision="fp64", seed=0, timed=False, fault=None):
+    from gqmap_opticalflow_amd import Engine
+    with _policy(flow=1 if flow else 0):
+        e = Engine(o, I1, I2, "mixture", precision)
+    try:
+        e.init_state(seed)
+        if fault is not None:
+            _inject(e, fault)
+        if timed:
+            done, _, kms = e.run_timed(its)
+            tr = None
+        else:
+            done, tr = e.run(its)
+        return done, tr, e.get_state()
+    finally:
+        e.close()
+
+
+def _inject(e, j):
+    import ctypes as C
+    from gqmap_opticalflow_amd import _lib
+    f = _lib.load().gqmap_debug_persist_fault
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_int]
+    assert f(e.ctx, j) == 0
+
+
+def _same(a, b):
+    for k in G.STATE_KEYS:
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+    assert a.it == b.it and a.T == b.T
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_flow_c2_bit_exact_vs_per_launch(precision):
+    """The full C2 frame, 133 iterations (two 50-iteration graph chunks, a
+    leftover of 33 as one launch): trace and state equal the per-launch
+    path's, and run_timed through the dataflow launches ends in the same
+    state."""
+    I1, I2, o = _c2()
+    d0, t0, s0 = _run(o, I1, I2, 133, False, precision)
+    d1, t1, s1 = _run(o, I1, I2, 133, True, precision)
+    assert d0 == d1 == 133
+    np.testing.assert_array_equal(t1, t0)
+    _same(s1, s0)
+    d2, _, s2 = _run(o, I1, I2, 133, True, precision, timed=True)
+    assert d2 == 133
+    _same(s2, s0)
+
+
+def test_flow_temperature_decay_bit_exact():
+    """T != 0 with a decay every 7 iterations: each workgroup replays the
+    decay up to its item's iteration as fin_apply applies it."""
+    I1, I2, o = _c2()
+    o = dict(o, temperature=0.3, t_decay_every=7)
+    d0, t0, s0 = _run(o, I1, I2, 61, False)
+    d1, t1, s1 = _run(o, I1, I2, 61, True)
+    np.testing.assert_array_equal(t1, t0)
+    _same(s1, s0)
+
+
+@pytest.mark.parametrize("k", [0, 1, 23, 48, 49, 57])
+def test_flow_stop_rule_anywhere_in_a_chunk(k):
+    """The stop rule met at iteration k (launch-local row k of a 50-iteration
+    chunk, or of the leftover launch): items of iteration k + 1 may already
+    have run (they wrote the buffer of state k - 1), later ones see the stop
+    word and leave; state, trace and stop iteration are the per-launch
+    path's."""
+    I1, I2, o = _c2()
+    _, tr, _ = _run(o, I1, I2, 70, False)
+    tor = 1e9 if k == 0 else float(tr[k, 1]) * (1 + 1e-12)
+    k = int(np.argmax(tr[:, 1] < tor))
+    o = dict(o, tor=tor)
+    d0, t0, s0 = _run(o, I1, I2, 70, False)
+    d1, t1, s1 = _run(o, I1, I2, 70, True)
+    assert d0 == d1 == k + 1
+    np.testing.assert_array_equal(t1, t0)
+    _same(s1, s0)
+
+
+@pytest.mark.parametrize("j", [0, 7, 49])
+def test_flow_failed_launch_recovers_bit_exact(j):
+    """A dataflow launch that gives up (the failure word raised at the first
+    item of iteration j, as a spin timeout raises it) leaves the state the
+    chunk started from to the host, which restores it and finishes with one
+    launch per iteration: the per-launch path's bits."""
+    I1, I2, o = _c2()
+    d0, t0, s0 = _run(o, I1, I2, 80, False)
+    d1, t1, s1 = _run(o, I1, I2, 80, True, fault=j)
+    assert d1 == 80
+    np.testing.assert_array_equal(t1, t0)
+    _same(s1, s0)
