@@ -1691,13 +1691,17 @@ __device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, u
 #ifndef GQ_FLOW_COH  // device-coherent state access (0: plain -- timing experiments only, not coherent)
 #define GQ_FLOW_COH 1
 #endif
-#ifndef GQ_FLOW_PREFETCH  // claim the next item while the current one runs
-#define GQ_FLOW_PREFETCH 1
+#ifndef GQ_FLOW_PREFETCH  // claim the next item while the current one runs (measured: +18%, reservation skew)
+#define GQ_FLOW_PREFETCH 0
 #endif
-template <typename R, typename VT>
-__global__ __launch_bounds__(BLOCK, GQ_FLOW_WAVES) void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles,
-                                                        const Ctl *snap)
+#ifndef GQ_FLOW_PAIR  // the next claim issued together with the arrival ticket (one round trip)
+#define GQ_FLOW_PAIR 0
+#endif
+template <typename R, typename VT, int ENG, int Q>
+__global__ __launch_bounds__(BLOCK, Q == 1 ? GQ_FLOW_WAVES : min_waves(ENG, Q))
+void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, const Ctl *snap)
 {
+    static_assert(ENG != 1 && Q >= 1 && Q <= 4, "single-pixel engines, 1..4 lanes per node");
     unsigned *bar = P.bar;
     // a stopped run, or a failed launch earlier in the replay (whose
     // snapshot the host restores): nothing to do but take the exit ticket
@@ -1709,8 +1713,9 @@ __global__ __launch_bounds__(BLOCK, GQ_FLOW_WAVES) void k_iter_flow(IterParams<R
     int s0 = 0;
     for (int y = 0; y < xcd; ++y) s0 += (ntiles - y + 7) >> 3;
     const int nb = (ntiles - xcd + 7) >> 3;  // this XCD's band: tiles [s0, s0 + nb)
-    const bool edge_first = GQ_FLOW_MIX && ((((b >> 3) / P.cu_slots) & 1) != GQ_PHASE_MIX_OTHER_INV);
-    __shared__ TileLdsQ<R, 1> lds;
+    constexpr int INV = ENG == 2 && Q == 1 ? GQ_PHASE_MIX_CTF_Q1_INV : GQ_PHASE_MIX_OTHER_INV;
+    const bool edge_first = GQ_FLOW_MIX && ((((b >> 3) / P.cu_slots) & 1) != INV);
+    __shared__ TileLdsQ<R, Q> lds;
     __shared__ int sh_i, sh_go, sh_last;
     __shared__ double tot[NFIX + GQMAP_LMAX];
     __shared__ unsigned long long sh_acc[4 * (NFIX + GQMAP_LMAX)];
@@ -1719,8 +1724,9 @@ __global__ __launch_bounds__(BLOCK, GQ_FLOW_WAVES) void k_iter_flow(IterParams<R
     unsigned nxt = 0;  // thread 0: the claim issued during the previous item
     if (run && nb > 0 && GQ_FLOW_PREFETCH && threadIdx.x == 0)
         nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool have = false;  // GQ_FLOW_PAIR: sh_i already holds the next claim
     while (run && nb > 0) {
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == 0 && !(GQ_FLOW_PAIR && have)) {
             if (GQ_FLOW_PREFETCH) {
                 sh_i = (int)nxt;
                 // the next claim goes out now; its latency hides behind this
@@ -1742,17 +1748,20 @@ __global__ __launch_bounds__(BLOCK, GQ_FLOW_WAVES) void k_iter_flow(IterParams<R
                 if (q % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
         unsigned long long *slot = acc + (size_t)(j & 1) * FL_ACC_SLOT;
         if (GQ_FLOW_MIX && edge_first)
-            iter_tile<R, VT, 0, 1, true, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
+            iter_tile<R, VT, ENG, Q, true, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
         else
-            iter_tile<R, VT, 0, 1, false, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
+            iter_tile<R, VT, ENG, Q, false, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
         // publish: every wave's stores (state, rou, the slot's sums) are done
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
             __hip_atomic_store(fl + FL_DONE + tile, (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh_last = __hip_atomic_fetch_add(fl + FL_ARR + (j & 1) * FL_LINE, 1u, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ntiles - 1);
+            const unsigned tk = __hip_atomic_fetch_add(fl + FL_ARR + (j & 1) * FL_LINE, 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (GQ_FLOW_PAIR) sh_i = (int)__hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sh_last = tk == (unsigned)(ntiles - 1);
         }
+        have = true;
         __syncthreads();
         if (sh_last) flow_finalize(P.fin, fl, bar, slot, j, tot, sh_acc, &sh_go);
         __syncthreads();
@@ -3129,8 +3138,8 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
 void drop_graph(gqmap_ctx *c);
 
 // ---- dataflow launch (k_iter_flow, policy flow) ---------------------------
-template <typename R, typename VT>
-bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
+template <typename R, typename VT, int ENG, int Q>
+bool launch_flow_q(gqmap_ctx *c, int n, bool dry)
 {
     const int ntiles = c->tiles_m * c->tiles_n;
     if (c->flow_n != flow_words(ntiles)) {  // (re)allocate outside any capture
@@ -3158,22 +3167,41 @@ bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
                                                        (const R *)c->d_st[1], (R *)c->d_snap, c->d_snap_ctl, nv);
     }
     IterParams<R, VT> P = iter_params<R, VT>(c);
-    static const int2 shape = kernel_shape(k_iter_flow<R, VT>);
+    static const int2 shape = kernel_shape(k_iter_flow<R, VT, ENG, Q>);
     P.cu_group = 1;
     P.cu_slots = std::max(1, shape.y / 8);
     // one workgroup per resident slot (more would only queue behind them)
     const int G = std::max(8, std::min(shape.x * shape.y, ntiles));
-    k_iter_flow<R, VT><<<G, BLOCK, 0, c->stream>>>(P, n, c->d_flow, ntiles, c->d_snap_ctl);
+    k_iter_flow<R, VT, ENG, Q><<<G, BLOCK, 0, c->stream>>>(P, n, c->d_flow, ntiles, c->d_snap_ctl);
     return true;
 }
 
+// Instantiated for the whole-grid single-scale mixture at Q = 1 (C2, either
+// precision) and the fp64 coarse-to-fine levels at Q = 1, 2, 4 (C3's 480x640,
+// 240x320, 120x160; the smaller ones run k_iter_persist).
+template <typename R, typename VT>
+bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
+{
+    if (c->opt.engine != GQMAP_ENGINE_CTF) return c->kq == 1 && launch_flow_q<R, VT, 0, 1>(c, n, dry);
+    if constexpr (sizeof(R) == 8) {
+        switch (c->kq) {
+        case 1: return launch_flow_q<R, VT, 2, 1>(c, n, dry);
+        case 2: return launch_flow_q<R, VT, 2, 2>(c, n, dry);
+        case 4: return launch_flow_q<R, VT, 2, 4>(c, n, dry);
+        default: return false;
+        }
+    }
+    return false;
+}
+
 // n iterations as one k_iter_flow launch when the policy asks for it and the
-// context qualifies (single-scale mixture, L = 1, one lane per node, the
-// whole grid, fast arithmetic); dry: only the check (and the buffers).
+// context qualifies (single-scale mixture at one lane per node, or an fp64
+// coarse-to-fine level at 1, 2 or 4; L = 1, the whole grid, fast
+// arithmetic); dry: only the check (and the buffers).
 bool launch_flow(gqmap_ctx *c, int n, bool dry)
 {
-    if (!c->pol.flow || c->persist_off || c->opt.engine != GQMAP_ENGINE_MIXTURE || c->L != 1 || c->n_tiles != 1 ||
-        c->comm || c->nranks != 0 || !fused_finalize(c) || c->kq != 1 || c->lit || n < 1)
+    if (!c->pol.flow || c->persist_off || c->opt.engine == GQMAP_ENGINE_SUPER || c->L != 1 || c->n_tiles != 1 ||
+        c->comm || c->nranks != 0 || !fused_finalize(c) || c->lit || n < 1)
         return false;
     if (c->fp32) return launch_flow_t<float, float>(c, n, dry);
     if (c->vv32) return launch_flow_t<double, vvs_t>(c, n, dry);

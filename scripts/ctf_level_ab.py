@@ -6,6 +6,10 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _policy  # noqa: E402  (GQMAP_POLICY="flow=1", ...)
+
+_policy.apply()
 import numpy as np  # noqa: E402
 
 from bench import gt_options  # noqa: E402

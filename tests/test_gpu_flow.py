@@ -117,3 +117,61 @@ def test_flow_failed_launch_recovers_bit_exact(j):
     assert d1 == 80
     np.testing.assert_array_equal(t1, t0)
     _same(s1, s0)
+
+
+@pytest.mark.parametrize("scale,q", [(1.0, 1), (0.5, 2), (0.25, 4)])
+def test_flow_ctf_levels_bit_exact(scale, q):
+    """The coarse-to-fine levels the dataflow launch takes (fp64, L = 1):
+    Grove3 at full resolution (Q = 1), 240 x 320 (Q = 2) and 120 x 160
+    (Q = 4, its table staged in LDS per item), with the truth set (the
+    AEPE trace of gqmap_ctf.m:38): trace, AEPE and state equal the
+    per-launch path's over 61 iterations."""
+    from gqmap_opticalflow_amd import Engine, ctf_options, flow_to_color, flowio, imresize
+    I1, I2, gt = flowio.load_pair("Grove3")
+    _, flo, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
+    if scale != 1.0:
+        I1, I2 = imresize(I1, scale), imresize(I2, scale)
+    o = ctf_options(its=61, minu=minu * scale, maxu=maxu * scale, minv=minv * scale, maxv=maxv * scale)
+    out = []
+    for flow in (0, 1):
+        with _policy(flow=flow):
+            e = Engine(o, I1, I2, "ctf")
+        try:
+            assert e.info().split == q
+            e.set_truth(np.asfortranarray(flo * scale))
+            e.init_state(3)
+            done, tr, ae = e.run_aepe(61)
+            out.append((done, tr, ae, e.get_state()))
+        finally:
+            e.close()
+    (d0, t0, a0, s0), (d1, t1, a1, s1) = out
+    assert d0 == d1 == 61
+    np.testing.assert_array_equal(t1, t0)
+    np.testing.assert_array_equal(a1, a0)
+    _same(s1, s0)
+
+
+def test_flow_c3_pyramid_same_flow():
+    """BASELINE C3 (Grove3, 5 levels) with every qualifying level on the
+    dataflow launch: the final flow and every level's intermediates equal
+    the per-launch pyramid's."""
+    from gqmap_opticalflow_amd import C3_SCALES, Pyramid, ctf_options, flow_to_color, flowio
+    I1, I2, gt = flowio.load_pair("Grove3")
+    _, _, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
+    opts = ctf_options(its=40, minu=minu, maxu=maxu, minv=minv, maxv=maxv)
+    res = []
+    for flow in (0, 1):
+        with _policy(flow=flow):
+            p = Pyramid(opts, C3_SCALES)
+            p.set_images(I1, I2)
+        try:
+            f, its, _ = p.run(seed=5)
+            res.append((f, its, [p.level(l) for l in range(len(C3_SCALES))]))
+        finally:
+            p.close()
+    (f0, i0, l0), (f1, i1, l1) = res
+    assert i0 == i1
+    np.testing.assert_array_equal(f1, f0)
+    for a, b in zip(l0, l1):
+        for k in ("I1w", "I2", "flow", "warp"):
+            np.testing.assert_array_equal(b[k], a[k], err_msg=k)
