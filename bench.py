@@ -492,6 +492,7 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
         a = aepe(flo, mp, unk)
     nodes = eng.M * eng.N
     split = eng.info().split
+    dataflow = eng.dataflow()
     # the flow after each of the first track_its iterations (the parity
     # gate's divergence trajectory against the literal restatement)
     maps_it = []
@@ -513,7 +514,10 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, instrumented_ms=total_ms, pixels=Mo * No, nodes=nodes, aepe=a, name=name,
                 settle=settle, maps_it=maps_it, literal=lit,
                 I1=I1, I2=I2, opts=opts, Mo=Mo, No=No, map=mpg, gate_its=gate_its, map1=mp1, flo=flo, unk=unk, split=split, seed=rank,
-                kernel=f"gq::k_iter<{R},float,{ksuf},Q> (VV stored as float: integer frames)",
+                kernel=(f"gq::k_iter_flow<{R},float,{ksuf},1> (dataflow launch: one per 50-iteration chunk, the "
+                        f"per-iteration average; VV stored as float)" if dataflow else
+                        f"gq::k_iter<{R},float,{ksuf},Q> (VV stored as float: integer frames)"),
+                dataflow=dataflow,
                 workload=f"{label}: {name} {No}x{Mo} {engine} L={L} K={K} its={args.steps} "
                          f"(one step = one full-frame iteration)")
 
@@ -1074,8 +1078,14 @@ def main():
                                        r.get("kernel", "gq::k_iter"))
             if "instrumented_ms" in r:
                 out["roofline"]["kernel_timing"] = (
-                    "HIP events around every k_iter launch in a replay of the timed iterations from the same "
-                    "initial state (bit-identical final state checked); the timed region itself is gqmap_run")
+                    ("HIP events around every dataflow launch (k_iter_flow: one launch per <= 50-iteration chunk) "
+                     "in a replay of the timed iterations from the same initial state (bit-identical final state "
+                     "checked), summed and divided by the iterations: kernel_avg_us is per iteration, and a "
+                     "rocprofv3 duration of k_iter_flow divided by the iterations of its launch compares with it"
+                     if r.get("dataflow") else
+                     "HIP events around every k_iter launch in a replay of the timed iterations from the same "
+                     "initial state (bit-identical final state checked)") + "; the timed region itself is gqmap_run")
+                out["roofline"]["dataflow"] = bool(r.get("dataflow"))
                 out["ms_per_step_instrumented"] = r["instrumented_ms"] / args.steps
         if tiled:
             out["per_pair"] = [{k: p[k] for k in ("name", "size", "aepe", "elapsed")} for p in r["per_pair"]]

@@ -2084,7 +2084,7 @@ struct Policy {
     int persist = 1;       // persistent launch of the small ctf levels
     int persist_cap = -1;  // resident workgroups assumed by the persistent launch (-1: occupancy query)
     int graph = 1;         // replayed hipGraphs (0: direct launches)
-    int flow = 0;          // dataflow launch of the single-scale engine (k_iter_flow; opt-in)
+    int flow = -1;         // dataflow launch (k_iter_flow): -1 auto (fp64 whole grids at Q = 1, 2, 4), 0 off, 1 on
     int vv_float = 1;      // float padded-frame store when exact
     int verbose = 0;       // recovery messages on stderr
 };
@@ -3200,7 +3200,11 @@ bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
 // arithmetic); dry: only the check (and the buffers).
 bool launch_flow(gqmap_ctx *c, int n, bool dry)
 {
-    if (!c->pol.flow || c->persist_off || c->opt.engine == GQMAP_ENGINE_SUPER || c->L != 1 || c->n_tiles != 1 ||
+    // auto: fp64 only -- the fp32 mixture kernel (4 waves per SIMD, gather
+    // latency-bound) measured slower as items (110.5 vs 107.9 us/it,
+    // profiles/r06_flow_ab_v1.txt)
+    const bool on = c->pol.flow > 0 || (c->pol.flow < 0 && !c->fp32);
+    if (!on || c->persist_off || c->opt.engine == GQMAP_ENGINE_SUPER || c->L != 1 || c->n_tiles != 1 ||
         c->comm || c->nranks != 0 || !fused_finalize(c) || c->lit || n < 1)
         return false;
     if (c->fp32) return launch_flow_t<float, float>(c, n, dry);
@@ -4086,6 +4090,15 @@ gqmap_status gqmap_debug_persist_fault(gqmap_ctx *c, int j)
 // the persistent launch to one launch per iteration.
 int gqmap_debug_persist_off(const gqmap_ctx *c) { return c && c->persist_off ? 1 : 0; }
 
+// Not in the public header (bench, tests): 1 when the context's runs take
+// the dataflow launch (k_iter_flow) -- allocates its queue buffer if needed.
+int gqmap_debug_flow(gqmap_ctx *c)
+{
+    if (!c || !c->have_images) return 0;
+    DeviceGuard dg(c->device);
+    return launch_flow(c, 1, true) ? 1 : 0;
+}
+
 // Not in the public header (tests, A/B scripts): set one execution policy of
 // gq::Policy by name, process-wide; contexts created (or graphs captured)
 // afterwards use it.  value -1 restores the automatic choice where there is
@@ -4100,7 +4113,7 @@ int gqmap_debug_policy(const char *name, int value)
         {"lpar_xcd", &g_pol.lpar_xcd, 1},    {"fused_finalize", &g_pol.fused_finalize, 1},
         {"persist", &g_pol.persist, 1},      {"persist_cap", &g_pol.persist_cap, -1},
         {"graph", &g_pol.graph, 1},          {"vv_float", &g_pol.vv_float, 1},
-        {"verbose", &g_pol.verbose, 0},      {"flow", &g_pol.flow, 0},
+        {"verbose", &g_pol.verbose, 0},      {"flow", &g_pol.flow, -1},
     };
     for (const Field &f : fields)
         if (std::strcmp(f.n, name) == 0) {

@@ -241,6 +241,15 @@ class Engine:
         """Build and upload the replayed iteration graph now (gqmap_prepare)."""
         check(self.lib.gqmap_prepare(self.ctx), "gqmap_prepare")
 
+    def dataflow(self) -> bool:
+        """Whether runs take the dataflow launch (k_iter_flow, one launch per
+        50-iteration chunk) rather than one k_iter launch per iteration
+        (gqmap_debug_flow; the library's flow policy)."""
+        f = self.lib.gqmap_debug_flow
+        f.restype = C.c_int
+        f.argtypes = [C.c_void_p]
+        return bool(f(self.ctx))
+
     def synchronize(self) -> None:
         check(self.lib.gqmap_synchronize(self.ctx), "gqmap_synchronize")
 
