@@ -1686,7 +1686,7 @@ __device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, u
 #define GQ_FLOW_WAVES 3
 #endif
 #ifndef GQ_FLOW_MIX  // node-first / edge-first alternation among co-resident workgroups
-#define GQ_FLOW_MIX 0
+#define GQ_FLOW_MIX 1
 #endif
 #ifndef GQ_FLOW_COH  // device-coherent state access (0: plain -- timing experiments only, not coherent)
 #define GQ_FLOW_COH 1
@@ -1696,6 +1696,14 @@ __device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, u
 #endif
 #ifndef GQ_FLOW_PAIR  // the next claim issued together with the arrival ticket (one round trip)
 #define GQ_FLOW_PAIR 0
+#endif
+// Each XCD queue walks its band row by row (band_row_tile) instead of down
+// the tile columns: a tile's left / right neighbours are then one queue
+// position away instead of a tile column (C2: 25 positions), so the items
+// of iteration j + 1 rarely find a neighbour of iteration j still running
+// (about 96 items are in flight per XCD against a band of 116).
+#ifndef GQ_FLOW_ROWS
+#define GQ_FLOW_ROWS 1
 #endif
 template <typename R, typename VT, int ENG, int Q>
 __global__ __launch_bounds__(BLOCK, Q == 1 ? GQ_FLOW_WAVES : min_waves(ENG, Q))
@@ -1714,7 +1722,7 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
     for (int y = 0; y < xcd; ++y) s0 += (ntiles - y + 7) >> 3;
     const int nb = (ntiles - xcd + 7) >> 3;  // this XCD's band: tiles [s0, s0 + nb)
     constexpr int INV = ENG == 2 && Q == 1 ? GQ_PHASE_MIX_CTF_Q1_INV : GQ_PHASE_MIX_OTHER_INV;
-    const bool edge_first = GQ_FLOW_MIX && ((((b >> 3) / P.cu_slots) & 1) != INV);
+    const bool edge_first = GQ_FLOW_MIX && ENG == 0 && ((((b >> 3) / P.cu_slots) & 1) != INV);
     __shared__ TileLdsQ<R, Q> lds;
     __shared__ int sh_i, sh_go, sh_last;
     __shared__ double tot[NFIX + GQMAP_LMAX];
@@ -1739,7 +1747,7 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
         __syncthreads();
         const int i = sh_i, j = i / nb;
         if (j >= n_iter) break;
-        const int tile = s0 + i % nb;
+        const int tile = GQ_FLOW_ROWS ? band_row_tile(i % nb, s0, s0 + nb, P.tiles_m) : s0 + i % nb;
         if (!flow_wait(fl, bar, P.tiles_m, ntiles, tile, j, &sh_go)) break;
         const int it = it0 + j, parity = (done0 + j) & 1;
         double T = T0;  // fin_apply's temperature decay after each earlier iteration
@@ -1747,7 +1755,7 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
             for (int q = it0; q < it; ++q)
                 if (q % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
         unsigned long long *slot = acc + (size_t)(j & 1) * FL_ACC_SLOT;
-        if (GQ_FLOW_MIX && edge_first)
+        if (GQ_FLOW_MIX && ENG == 0 && edge_first)
             iter_tile<R, VT, ENG, Q, true, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
         else
             iter_tile<R, VT, ENG, Q, false, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
@@ -2084,7 +2092,7 @@ struct Policy {
     int persist = 1;       // persistent launch of the small ctf levels
     int persist_cap = -1;  // resident workgroups assumed by the persistent launch (-1: occupancy query)
     int graph = 1;         // replayed hipGraphs (0: direct launches)
-    int flow = -1;         // dataflow launch (k_iter_flow): -1 auto (fp64 whole grids at Q = 1, 2, 4), 0 off, 1 on
+    int flow = -1;         // dataflow launch (k_iter_flow): -1 auto (fp64 whole grids at Q = 1, 2), 0 off, 1 on
     int vv_float = 1;      // float padded-frame store when exact
     int verbose = 0;       // recovery messages on stderr
 };
@@ -3187,7 +3195,9 @@ bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
         switch (c->kq) {
         case 1: return launch_flow_q<R, VT, 2, 1>(c, n, dry);
         case 2: return launch_flow_q<R, VT, 2, 2>(c, n, dry);
-        case 4: return launch_flow_q<R, VT, 2, 4>(c, n, dry);
+        // Q = 4 (120x160: 300 tiles, all resident in one round -- no tail to
+        // fill) measured 48.5 -> 51.5 us/it as items: only when forced
+        case 4: return c->pol.flow > 0 && launch_flow_q<R, VT, 2, 4>(c, n, dry);
         default: return false;
         }
     }

@@ -15,6 +15,9 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# iterations per k_iter_flow dispatch in the profiled run (FLOW_ITS=50 with
+# scripts/prof_iter.py and a multiple of 50 iterations; 0: not a flow profile)
+FLOW_ITS = int(os.environ.get("FLOW_ITS", "0"))
 
 
 def rows(path):
@@ -69,7 +72,21 @@ def main():
         lines.append(f"{name[:70]:70s} {r['Calls']:>6s} {float(r['AverageNs']) / 1e3:10.2f} "
                      f"{f if f is not None else float('nan'):12.1f} {w if w is not None else float('nan'):12.1f} "
                      f"{(corr or float('nan')) / 1e6:13.3f}")
-        if cfg != "c1" and "k_iter" in name and traffic is None and corr is not None:
+        if cfg != "c1" and "k_iter_flow" in name and corr is not None and FLOW_ITS:
+            # the dataflow launch runs FLOW_ITS iterations per dispatch in the
+            # profiled driver (scripts/prof_iter.py with a multiple of 50):
+            # per-iteration figures, comparable with a per-launch k_iter's
+            # (durations: the stats come from the bench trace, whose dispatches
+            # run different iteration counts -- per-iteration times are in the
+            # trace_segments.py table instead)
+            traffic = dict(kernel=name, iterations_per_launch=FLOW_ITS, avg_us=None, fetch_kb=f / FLOW_ITS,
+                           write_kb=w / FLOW_ITS, fetch_corr=fcorr, write_corr=wcorr,
+                           hbm_bytes_per_launch=corr / FLOW_ITS, unit="HBM bytes per iteration",
+                           source=f"profiles/{tag}_{cfg}_{prec}_summary.txt")
+            lines.append(f"  -> counters per iteration ({FLOW_ITS} iterations per dispatch in the counter passes): "
+                         f"FETCH {f / FLOW_ITS:.1f} KB, WRITE {w / FLOW_ITS:.1f} KB, HBM {corr / FLOW_ITS / 1e6:.3f} MB "
+                         f"(the avg_us column: the bench trace's dispatches, of mixed iteration counts)")
+        elif cfg != "c1" and "k_iter" in name and "k_iter_flow" not in name and traffic is None and corr is not None:
             traffic = dict(kernel=name, avg_us=float(r["AverageNs"]) / 1e3, fetch_kb=f, write_kb=w,
                            fetch_corr=fcorr, write_corr=wcorr, hbm_bytes_per_launch=corr,
                            source=f"profiles/{tag}_{cfg}_{prec}_summary.txt")
