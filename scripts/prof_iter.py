@@ -18,6 +18,12 @@ engine = sys.argv[3] if len(sys.argv) > 3 else "mixture"
 if engine == "super":
     I1, I2, flo, unk, o = setup_problem("Urban3", 3, 11)
     o.update(temperature=0.2, drate=0.75, lambdas=16.0)
+elif os.environ.get("GQMAP_SCALE"):  # a C5 frame: RubberWhale upsampled (optical_flow_temp.m:7-8)
+    from gqmap_opticalflow_amd import flow_to_color, flowio
+    I1, I2, gt = flowio.load_pair_scaled("rubberwhale", float(os.environ["GQMAP_SCALE"]))
+    _, flo, (minu, maxu, minv, maxv), unk = flow_to_color(gt)
+    o = dict(K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdas=5.0, lambdad=1.0,
+             minu=minu, maxu=maxu, minv=minv, maxv=maxv)
 else:
     I1, I2, flo, unk, o = setup_problem("rubberwhale", 1, 9)
 if os.environ.get("GQMAP_SPLIT"):
