@@ -883,7 +883,9 @@ __device__ __forceinline__ void iter_tile(const IterParams<R, VT> P, int tile, i
     const bool halo_lane = rtid < HALO_LANES;
 
     for (int l = l0; l < l1; ++l) {
-        const R a = R(ctl->alpha[l]);
+        // (COH: the dataflow kernel, whose alpha a finalize on another XCD
+        // may just have updated)
+        const R a = R(COH ? __hip_atomic_load(&ctl->alpha[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ctl->alpha[l]);
         const int64_t i = m + (int64_t)M * n + MN * l;
         // mu_u, mu_v, sigma_u, sigma_v, pn of the node; the four rou planes
         // are read and updated by their edge jobs.  (Named scalars, not an
@@ -1598,8 +1600,12 @@ constexpr int flow_words(int ntiles) { return FL_DONE + ntiles; }
 // Wait (wave 0 polls, the workgroup follows) until item (j, tile) may run.
 // Returns 1: run it; 0: leave (the run stopped before iteration j - 1, or a
 // failure -- injected, another workgroup's, or this spin's own timeout).
-__device__ __forceinline__ int flow_wait(unsigned *fl, unsigned *bar, int tiles_m, int ntiles, int tile, int j,
-                                         int *sh)
+// Per-tile counters are per (tile, component) item: index tile * L + l (the
+// super engine's mixture components are separate items, L > 1).  fin_need:
+// the finalized count item j needs -- j - 1 normally (iterations up to
+// j - 2), j when finalize(j - 1) updated alpha (L > 1 past alpha_start).
+__device__ __forceinline__ int flow_wait(unsigned *fl, unsigned *bar, int tiles_m, int ntiles, int tile, int l,
+                                         int L, int j, int fin_need, int *sh)
 {
     if (threadIdx.x < 64) {
         const int x = threadIdx.x;
@@ -1612,12 +1618,13 @@ __device__ __forceinline__ int flow_wait(unsigned *fl, unsigned *bar, int tiles_
             else if (x == 3 && tile >= tiles_m) dep = tile - tiles_m;
             else if (x == 4 && tile + tiles_m < ntiles) dep = tile + tiles_m;
         }
+        if (dep >= 0) dep = dep * L + l;
         unsigned spins = 0;
         int go = 1;
         while (true) {
             bool ok = true, leave = false;
             if (dep >= 0) ok = __hip_atomic_load(fl + FL_DONE + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)j;
-            else if (x == 5 && j >= 2) ok = __hip_atomic_load(fl + FL_FIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)(j - 1);
+            else if (x == 5 && fin_need > 0) ok = __hip_atomic_load(fl + FL_FIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)fin_need;
             else if (x == 6) {
                 const unsigned st = __hip_atomic_load(fl + FL_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 leave = st != 0 && (int)st - 1 <= j - 2;
@@ -1705,11 +1712,12 @@ __device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, u
 #ifndef GQ_FLOW_ROWS
 #define GQ_FLOW_ROWS 1
 #endif
-template <typename R, typename VT, int ENG, int Q>
-__global__ __launch_bounds__(BLOCK, Q == 1 ? GQ_FLOW_WAVES : min_waves(ENG, Q))
+template <typename R, typename VT, int ENG, int Q, bool LIT = false>
+__global__ __launch_bounds__(BLOCK, Q == 1 ? GQ_FLOW_WAVES : ENG == 1 ? 2 : min_waves(ENG, Q))
 void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, const Ctl *snap)
 {
-    static_assert(ENG != 1 && Q >= 1 && Q <= 4, "single-pixel engines, 1..4 lanes per node");
+    static_assert(Q >= 1 && Q <= 4, "1..4 lanes per node");
+    static_assert(!LIT || (ENG == 0 && Q == 1), "literal order: the mixture engine at one lane per node");
     unsigned *bar = P.bar;
     // a stopped run, or a failed launch earlier in the replay (whose
     // snapshot the host restores): nothing to do but take the exit ticket
@@ -1721,8 +1729,14 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
     int s0 = 0;
     for (int y = 0; y < xcd; ++y) s0 += (ntiles - y + 7) >> 3;
     const int nb = (ntiles - xcd + 7) >> 3;  // this XCD's band: tiles [s0, s0 + nb)
+    // items per tile and iteration: one per mixture component for the super
+    // engine (its node grid is small; a tile's components run back to back
+    // in the queue), one otherwise (L = 1)
+    const int L = ENG == 1 ? P.L : 1, nbl = nb * L, nitems = ntiles * L;
     constexpr int INV = ENG == 2 && Q == 1 ? GQ_PHASE_MIX_CTF_Q1_INV : GQ_PHASE_MIX_OTHER_INV;
-    const bool edge_first = GQ_FLOW_MIX && ENG == 0 && ((((b >> 3) / P.cu_slots) & 1) != INV);
+    // (the phase mix: the fast mixture engine only -- the literal kernel's
+    // second instantiation would spill)
+    const bool edge_first = GQ_FLOW_MIX && ENG == 0 && !LIT && ((((b >> 3) / P.cu_slots) & 1) != INV);
     __shared__ TileLdsQ<R, Q> lds;
     __shared__ int sh_i, sh_go, sh_last;
     __shared__ double tot[NFIX + GQMAP_LMAX];
@@ -1739,35 +1753,38 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
                 sh_i = (int)nxt;
                 // the next claim goes out now; its latency hides behind this
                 // item's first state loads (a claim past the last item is harmless)
-                if ((int)nxt / nb < n_iter) nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((int)nxt / nbl < n_iter) nxt = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 sh_i = (int)__hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
-        const int i = sh_i, j = i / nb;
+        const int i = sh_i, j = i / nbl, pos = (i % nbl) / L, l = ENG == 1 ? i % L : 0;
         if (j >= n_iter) break;
-        const int tile = GQ_FLOW_ROWS ? band_row_tile(i % nb, s0, s0 + nb, P.tiles_m) : s0 + i % nb;
-        if (!flow_wait(fl, bar, P.tiles_m, ntiles, tile, j, &sh_go)) break;
+        const int tile = GQ_FLOW_ROWS ? band_row_tile(pos, s0, s0 + nb, P.tiles_m) : s0 + pos;
         const int it = it0 + j, parity = (done0 + j) & 1;
+        // finalize(j - 1) changed alpha (fin_apply: it - 1 > alpha_start, L > 1)
+        const bool alpha_moved = P.L > 1 && it - 1 > P.fin.alpha_start;
+        if (!flow_wait(fl, bar, P.tiles_m, ntiles, tile, l, L, j, alpha_moved ? j : j - 1, &sh_go)) break;
         double T = T0;  // fin_apply's temperature decay after each earlier iteration
         if (P.fin.t_decay_every > 0)
             for (int q = it0; q < it; ++q)
                 if (q % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
         unsigned long long *slot = acc + (size_t)(j & 1) * FL_ACC_SLOT;
-        if (GQ_FLOW_MIX && ENG == 0 && edge_first)
-            iter_tile<R, VT, ENG, Q, true, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
+        const int l0 = ENG == 1 ? l : 0, l1 = ENG == 1 ? l + 1 : 1;  // (L = 1 unless super)
+        if (GQ_FLOW_MIX && ENG == 0 && !LIT && edge_first)
+            iter_tile<R, VT, ENG, Q, true, GQ_FLOW_COH, false, LIT>(P, tile, it, parity, 0, lds, l0, l1, T, false, slot);
         else
-            iter_tile<R, VT, ENG, Q, false, GQ_FLOW_COH>(P, tile, it, parity, 0, lds, 0, 1, T, false, slot);
+            iter_tile<R, VT, ENG, Q, false, GQ_FLOW_COH, false, LIT>(P, tile, it, parity, 0, lds, l0, l1, T, false, slot);
         // publish: every wave's stores (state, rou, the slot's sums) are done
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
-            __hip_atomic_store(fl + FL_DONE + tile, (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(fl + FL_DONE + tile * L + l, (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned tk = __hip_atomic_fetch_add(fl + FL_ARR + (j & 1) * FL_LINE, 1u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
             if (GQ_FLOW_PAIR) sh_i = (int)__hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sh_last = tk == (unsigned)(ntiles - 1);
+            sh_last = tk == (unsigned)(nitems - 1);
         }
         have = true;
         __syncthreads();
@@ -1780,7 +1797,7 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
         sh_last = __hip_atomic_fetch_add(fl + FL_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (sh_last) {
-        for (int w = threadIdx.x; w < flow_words(ntiles); w += blockDim.x)
+        for (int w = threadIdx.x; w < flow_words(nitems); w += blockDim.x)
             __hip_atomic_store(fl + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -3146,25 +3163,26 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
 void drop_graph(gqmap_ctx *c);
 
 // ---- dataflow launch (k_iter_flow, policy flow) ---------------------------
-template <typename R, typename VT, int ENG, int Q>
+template <typename R, typename VT, int ENG, int Q, bool LIT = false>
 bool launch_flow_q(gqmap_ctx *c, int n, bool dry)
 {
     const int ntiles = c->tiles_m * c->tiles_n;
-    if (c->flow_n != flow_words(ntiles)) {  // (re)allocate outside any capture
+    const int nitems = ntiles * (ENG == 1 ? c->L : 1);  // items per iteration
+    if (c->flow_n != flow_words(nitems)) {  // (re)allocate outside any capture
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(c->stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
         if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
         if (c->d_flow) (void)hipFree(c->d_flow);
         c->d_flow = nullptr;
         c->flow_n = 0;
-        if (hipMalloc((void **)&c->d_flow, sizeof(unsigned) * flow_words(ntiles)) != hipSuccess) {
+        if (hipMalloc((void **)&c->d_flow, sizeof(unsigned) * flow_words(nitems)) != hipSuccess) {
             c->d_flow = nullptr;
             return false;
         }
-        if (hipMemsetAsync(c->d_flow, 0, sizeof(unsigned) * flow_words(ntiles), c->stream) != hipSuccess ||
+        if (hipMemsetAsync(c->d_flow, 0, sizeof(unsigned) * flow_words(nitems), c->stream) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess)
             return false;
-        c->flow_n = flow_words(ntiles);
+        c->flow_n = flow_words(nitems);
     }
     if (!ensure_snap(c)) return false;
     if (dry) return true;
@@ -3175,12 +3193,12 @@ bool launch_flow_q(gqmap_ctx *c, int n, bool dry)
                                                        (const R *)c->d_st[1], (R *)c->d_snap, c->d_snap_ctl, nv);
     }
     IterParams<R, VT> P = iter_params<R, VT>(c);
-    static const int2 shape = kernel_shape(k_iter_flow<R, VT, ENG, Q>);
+    static const int2 shape = kernel_shape(k_iter_flow<R, VT, ENG, Q, LIT>);
     P.cu_group = 1;
     P.cu_slots = std::max(1, shape.y / 8);
     // one workgroup per resident slot (more would only queue behind them)
-    const int G = std::max(8, std::min(shape.x * shape.y, ntiles));
-    k_iter_flow<R, VT, ENG, Q><<<G, BLOCK, 0, c->stream>>>(P, n, c->d_flow, ntiles, c->d_snap_ctl);
+    const int G = std::max(8, std::min(shape.x * shape.y, nitems));
+    k_iter_flow<R, VT, ENG, Q, LIT><<<G, BLOCK, 0, c->stream>>>(P, n, c->d_flow, ntiles, c->d_snap_ctl);
     return true;
 }
 
@@ -3190,7 +3208,25 @@ bool launch_flow_q(gqmap_ctx *c, int n, bool dry)
 template <typename R, typename VT>
 bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
 {
-    if (c->opt.engine != GQMAP_ENGINE_CTF) return c->kq == 1 && launch_flow_q<R, VT, 0, 1>(c, n, dry);
+    if (c->opt.engine == GQMAP_ENGINE_SUPER) {
+        // C4's node grid (120 x 160, L = 3) at Q = 4, a mixture component per
+        // item: bit-exact, but 283 -> 308 us/it (the per-launch kernel's
+        // 234 VGPRs become 255 with spills; profiles/r06_super_flow_ab.txt):
+        // only when forced
+        if constexpr (sizeof(R) == 8) return c->pol.flow > 0 && c->kq == 4 && launch_flow_q<R, VT, 1, 4>(c, n, dry);
+        return false;
+    }
+    if (c->opt.engine != GQMAP_ENGINE_CTF) {
+        if constexpr (sizeof(R) == 8 && sizeof(VT) == 4) {
+            // the literal-order arithmetic on integer frames (C2's parity-carrying
+            // engine): bit-exact as items, but its kernel sits at 167 VGPRs and
+            // the dataflow wrapper spills 20 (274.7 -> 283 us/it,
+            // profiles/r06_lit_flow_ab.txt): only when forced
+            if (c->lit) return c->pol.flow > 0 && c->kq == 1 && launch_flow_q<R, VT, 0, 1, true>(c, n, dry);
+        }
+        return !c->lit && c->kq == 1 && launch_flow_q<R, VT, 0, 1>(c, n, dry);
+    }
+    if (c->lit) return false;
     if constexpr (sizeof(R) == 8) {
         switch (c->kq) {
         case 1: return launch_flow_q<R, VT, 2, 1>(c, n, dry);
@@ -3214,8 +3250,8 @@ bool launch_flow(gqmap_ctx *c, int n, bool dry)
     // latency-bound) measured slower as items (110.5 vs 107.9 us/it,
     // profiles/r06_flow_ab_v1.txt)
     const bool on = c->pol.flow > 0 || (c->pol.flow < 0 && !c->fp32);
-    if (!on || c->persist_off || c->opt.engine == GQMAP_ENGINE_SUPER || c->L != 1 || c->n_tiles != 1 ||
-        c->comm || c->nranks != 0 || !fused_finalize(c) || c->lit || n < 1)
+    if (!on || c->persist_off || (c->L != 1 && c->opt.engine != GQMAP_ENGINE_SUPER) || c->n_tiles != 1 ||
+        c->comm || c->nranks != 0 || !fused_finalize(c) || n < 1)
         return false;
     if (c->fp32) return launch_flow_t<float, float>(c, n, dry);
     if (c->vv32) return launch_flow_t<double, vvs_t>(c, n, dry);

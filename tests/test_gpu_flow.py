@@ -175,3 +175,45 @@ def test_flow_c3_pyramid_same_flow():
     for a, b in zip(l0, l1):
         for k in ("I1w", "I2", "flow", "warp"):
             np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+
+
+def test_flow_literal_order_forced_bit_exact():
+    """The literal-order engine (arith = literal) on the dataflow launch when
+    forced (policy flow = 1; its default stays per launch): the per-launch
+    literal engine's bits over a graph chunk and a leftover."""
+    I1, I2, o = _c2()
+    o = dict(o, arith="literal", split=1)
+    d0, t0, s0 = _run(o, I1, I2, 61, False)
+    d1, t1, s1 = _run(o, I1, I2, 61, True)
+    assert d0 == d1 == 61
+    np.testing.assert_array_equal(t1, t0)
+    _same(s1, s0)
+
+
+@pytest.mark.parametrize("alpha_start,its", [(500, 61), (10, 61)])
+def test_flow_super_mixture_components_bit_exact(alpha_start, its):
+    """BASELINE C4 (Urban3, super engine, L = 3, K = 11, Q = 4): each mixture
+    component of a tile is its own item.  Past alpha_start the alpha update
+    of finalize(j - 1) feeds iteration j, so items then wait for it (lag 1
+    instead of 2); with the temperature decay every 15 iterations.  The
+    per-launch path's trace, alpha and state bit for bit."""
+    from gqmap_opticalflow_amd import Engine, flow_to_color, flowio
+    I1, I2, gt = flowio.load_pair("Urban3")
+    _, _, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
+    o = dict(K=11, L=3, temperature=0.2, drate=0.75, epsn=1e-6, lambdad=1.0, lambdas=16.0,
+             minu=minu, maxu=maxu, minv=minv, maxv=maxv, alpha_start=alpha_start, t_decay_every=15)
+    out = []
+    for flow in (0, 1):
+        with _policy(flow=flow):
+            e = Engine(o, I1, I2, "super")
+        try:
+            assert e.info().split == 4 and e.dataflow() == bool(flow)
+            e.init_state(4)
+            done, tr = e.run(its)
+            out.append((done, tr, e.get_state()))
+        finally:
+            e.close()
+    (d0, t0, s0), (d1, t1, s1) = out
+    assert d0 == d1 == its
+    np.testing.assert_array_equal(t1, t0)
+    _same(s1, s0)
