@@ -375,6 +375,13 @@ def traffic_per_launch(precision: str, config: str):
     return None
 
 
+def traffic_unit(precision: str, config: str):
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{config}_{precision}.json")
+    if not os.path.exists(tfile):
+        return None
+    return json.load(open(tfile)).get("unit", "HBM bytes per k_iter launch (one iteration)")
+
+
 def traffic_source(precision: str, config: str):
     tfile = os.path.join(ROOT, "profiles", f"traffic_{config}_{precision}.json")
     if not os.path.exists(tfile):
@@ -391,6 +398,7 @@ def roofline(engine, L, K, nodes, precision, kernel_avg_s, config, kernel_name):
     peak = PEAK_TFLOPS[precision]
     return {"bound": "valu", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
             "traffic": traffic_per_launch(precision, config), "traffic_source": traffic_source(precision, config),
+            "traffic_unit": traffic_unit(precision, config),
             "kernel": kernel_name,
             "kernel_avg_us": kernel_avg_s * 1e6, "flops_per_launch": fl,
             "algorithmic_bytes_per_launch": by, "hbm_algorithmic_GBps": by / kernel_avg_s / 1e9,
