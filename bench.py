@@ -939,6 +939,9 @@ def main():
                          "bit for bit against the literal restatement)")
     ap.add_argument("--tiled", action="store_true",
                     help="c2: strong scaling -- the RubberWhale pair split into column strips over the ranks")
+    ap.add_argument("--policy", default="",
+                    help="A/B only: library execution policies name=value,... (gqmap_debug_policy, e.g. flow=0 "
+                         "for one launch per iteration); they never change a result")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = DEFAULT_STEPS[args.config]
@@ -947,6 +950,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    if args.policy:  # (after torch: the library must bind to torch's HIP runtime)
+        from gqmap_opticalflow_amd import _lib
+        for item in args.policy.split(","):
+            name, _, value = item.partition("=")
+            _lib.debug_policy(name.strip(), int(value))
     dist = None
     # GQMAP_BENCH_BACKEND=gloo rehearses the multi-rank harness on a box with
     # fewer GPUs than ranks (ranks then share devices round-robin); the
@@ -1032,6 +1040,7 @@ def main():
             "data": "Middlebury frame10/11 + flow10.flo (real frames, in-repo data/middlebury)"
                     + ("; upsampled 4x on the device" if cfg == "c5" else ""),
             "config": {"workload": r["workload"], "engine": engine, "L": L, "K": K, "parallelism": parallel},
+            "policy": args.policy or "default",
             "aepe": r["aepe"], "aepe_its": args.steps,
             "timed_region": "iterations 1..steps of the solve (gqmap_gpu_mixture.m:27-50, 69-75 on the device); "
                             "the reference loop's host evaluation block (it==1 / every 300 its: MAP, PNG, AEPE, "
