@@ -1167,8 +1167,11 @@ __global__ __launch_bounds__(BLOCK, min_waves(ENG, Q)) void k_iter(IterParams<R,
 
 // The literal-order arithmetic (gqmap_options.arith = GQMAP_ARITH_LITERAL):
 // the same tiles, halo, update and finalize with lit_node_grad / lit_edge_grad.
+#ifndef GQ_LIT_WAVES  // waves per SIMD the literal kernel's allocation must allow (1: the allocator's choice)
+#define GQ_LIT_WAVES 3
+#endif
 template <typename VT, bool NT = false>
-__global__ __launch_bounds__(BLOCK, 1) void k_iter_lit(IterParams<double, VT> P)
+__global__ __launch_bounds__(BLOCK, GQ_LIT_WAVES) void k_iter_lit(IterParams<double, VT> P)
 {
     k_iter_body<double, VT, 0, 1, NT, true>(P);
 }

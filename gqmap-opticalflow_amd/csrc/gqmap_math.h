@@ -1127,6 +1127,59 @@ GQ_HD void lit_points(TP tab, int K2, const LitCoef &c, double p, LitAcc &S, PT 
 #endif
 }
 
+// Form 3 (GQ_LIT_MIRROR, edge gradients at K = 9): rows r and K-1-r of a
+// meshgrid column share A = XI^2+XJ^2, M = XI^2-XJ^2 and A - 1 exactly (the
+// library's Gauss-Hermite rule is symmetric: x(K-1-i) = -x(i), the middle
+// node 0 -- gauss_hermite), so the same p - p*A, the same division M/sqrtpr
+// and the same do-factors; XJ and 2*XI*XJ only flip sign.  The later row
+// reuses the earlier row's rounded values instead of recomputing them: the
+// same operations on the same operands as the per-point form, in the same
+// accumulation order.  The column's pending values live in registers (the
+// column loop fully unrolled).
+#ifndef GQ_LIT_MIRROR
+#define GQ_LIT_MIRROR 1
+#endif
+#ifndef GQ_LIT_MIRROR_NODE  // the same sharing in the node gradient's loop
+#define GQ_LIT_MIRROR_NODE 0
+#endif
+template <int KK, typename TP, typename PT>
+GQ_HD void lit_points_mirror(TP tab, const LitCoef &c, double p, LitAcc &S, PT pt)
+{
+    constexpr int H = KK / 2;
+    for (int cc = 0, k0 = 0; cc < KK; ++cc, k0 += KK) {
+        const double XI = tab[tab_at(TL_XI, k0)];
+        const double sXI = c.s * XI, tXI = c.t * XI;
+        double pA[H], F1[H], F2[H];
+#ifdef __HIPCC__
+#pragma unroll
+#endif
+        for (int r = 0; r < KK; ++r) {
+            const int k = k0 + r;
+            const double XJ = tab[tab_at(TL_XJ, k)];
+            const double zi = sXI + c.t * XJ, zj = tXI + c.s * XJ;
+            const double fval = pt(k, zi, zj);
+            double pa, f1, f2;
+            if (r <= H) {
+                pa = p - p * tab[tab_at(TL_A, k)];
+                const double q = div_rcp(tab[tab_at(TL_M, k)], c.sqrtpr, c.rsqrtpr);
+                f1 = tab[tab_at(TL_A1, k)] + q;
+                f2 = tab[tab_at(TL_A1, k)] - q;
+                if (r < H) { pA[r] = pa; F1[r] = f1; F2[r] = f2; }
+            } else {
+                pa = pA[KK - 1 - r];
+                f1 = F1[KK - 1 - r];
+                f2 = F2[KK - 1 - r];
+            }
+            S.dp = S.dp + fval * (pa + tab[tab_at(TL_X2, k)]);
+            S.du1 = S.du1 + fval * (zi - p * zj);
+            S.du2 = S.du2 + fval * (zj - p * zi);
+            S.do1 = S.do1 + fval * f1;
+            S.do2 = S.do2 + fval * f2;
+            S.Ei = S.Ei + fval;
+        }
+    }
+}
+
 template <typename TP, typename PT>
 GQ_HD void lit_points_dyn(TP tab, int K2, const LitCoef &c, double p, LitAcc &S, PT pt, bool live)
 {
@@ -1173,11 +1226,16 @@ GQ_HD Grad<double> lit_node_grad(TP tab, int K2, VP VV, int M2, IP I1, int Mo, i
     const double I = I1[m + (int64_t)Mo * n];
     const bool live = !guard || a != 0;
     LitAcc S;
-    lit_loop(tab, K2, c, p, live, S, [&](int k, double zi, double zj) {
+    auto pt = [&](int k, double zi, double zj) {
         const double x1 = so1 * zi + u1, x2 = so2 * zj + u2;
         const double d = I - lit_interp(VV, M2, Mo, No, (double)(n + 1) + x1, (double)(m + 1) + x2);
         return tab[tab_at(TL_W, k)] * (-lamd * GQ_SQRT(eps + d * d));
-    });
+    };
+#if GQ_LIT_MIRROR && GQ_LIT_MIRROR_NODE
+    if (K2 == 81 && live) lit_points_mirror<9>(tab, c, p, S, pt);
+    else
+#endif
+        lit_loop(tab, K2, c, p, live, S, pt);
     return lit_epi(S, c, a, o1, o2, p, T, true);
 }
 
@@ -1190,10 +1248,15 @@ GQ_HD Grad<double> lit_edge_grad(TP tab, int K2, double eps, double lams, bool g
     const double so1 = GQ_M_SQRT2 * o1, so2 = GQ_M_SQRT2 * o2;
     const bool live = !guard || a != 0;
     LitAcc S;
-    lit_loop(tab, K2, c, p, live, S, [&](int k, double zi, double zj) {
+    auto pt = [&](int k, double zi, double zj) {
         const double d = (so1 * zi + u1) - (so2 * zj + u2);
         return tab[tab_at(TL_W, k)] * (-lams * GQ_SQRT(eps + d * d));
-    });
+    };
+#if GQ_LIT_MIRROR
+    if (K2 == 81 && live) lit_points_mirror<9>(tab, c, p, S, pt);
+    else
+#endif
+        lit_loop(tab, K2, c, p, live, S, pt);
     return lit_epi(S, c, a, o1, o2, p, T, false);
 }
 

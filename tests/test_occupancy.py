@@ -39,13 +39,18 @@ LIMITS = {
     "_ZN2gq10k_iter_litIfLb1EEEvNS_10IterParamsIdT_EE": 168,
 }
 # kernels that must run without a private (scratch) segment: the C2 kernels
-# of both arithmetics (round 5's literal kernel carried 20 bytes of it)
+# of the fast arithmetic; the literal kernel is held to 3 waves by its launch
+# bound (GQ_LIT_WAVES) and may spill a few registers there -- measured faster
+# than the 174-VGPR, 2-wave allocation (profiles/r06_lit_mirror_ab.txt) --
+# but not more than SCRATCH_MAX bytes
 NO_SCRATCH = (
     "_ZN2gq6k_iterIdfLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
     "_ZN2gq6k_iterIffLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
-    "_ZN2gq10k_iter_litIfLb0EEEvNS_10IterParamsIdT_EE",
-    "_ZN2gq10k_iter_litIfLb1EEEvNS_10IterParamsIdT_EE",
 )
+SCRATCH_MAX = {
+    "_ZN2gq10k_iter_litIfLb0EEEvNS_10IterParamsIdT_EE": 128,
+    "_ZN2gq10k_iter_litIfLb1EEEvNS_10IterParamsIdT_EE": 128,
+}
 
 
 def _kernel_registers(tmp):
@@ -78,3 +83,5 @@ def test_headline_kernels_keep_their_waves(tmp_path):
         assert v <= limit and a == 0, f"{name}: {v} VGPRs + {a} AGPRs > {limit}"
     for name in NO_SCRATCH:
         assert regs[name][2] == 0, f"{name}: {regs[name][2]} bytes of scratch"
+    for name, mx in SCRATCH_MAX.items():
+        assert regs[name][2] <= mx, f"{name}: {regs[name][2]} bytes of scratch > {mx}"
