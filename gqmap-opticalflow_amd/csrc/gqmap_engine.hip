@@ -93,7 +93,13 @@ __device__ __forceinline__ float gq_sqrt_dev(float x)
 
 namespace gq {
 
-typedef float vvs_t;  // VV storage of the fp64 engine for integer-valued frames (exact)
+// VV storage of the fp64 engine for integer-valued frames (exact).  binary16
+// (exact too: C2's values lie in [-510, 765]) halves the tap-gather bytes but
+// needs two conversions per tap: C2 fast 141.7 -> 179.7 us/it, literal
+// 250.4 -> 267.7 (profiles/r06_vvh_ab.txt); double storage (policy
+// vv_float=0) drops the conversion but doubles the bytes and the tap
+// registers: literal 255 -> 296 (profiles/r06_lit_vv_ab.txt).
+typedef float vvs_t;
 
 constexpr int TILE = 16;
 constexpr int BLOCK = TILE * TILE;
@@ -126,7 +132,9 @@ struct Ctl {
     // has judged the stop rule on the all-gathered totals.  A cache line of
     // their own.  ovr: 1 + the sequence row whose totals met the stop rule
     // when later iterations of the sequence had already run (the host then
-    // restores the sequence's snapshot and re-runs it exactly, deferred_recover).
+    // restores the sequence's snapshot and re-runs it exactly, ovr_recover);
+    // also 1 + the launch-local stop iteration of a dataflow launch whose
+    // items ran two or more iterations past it (GQ_FLOW_LAG > 2).
     alignas(128) int it_i;
     int done_i;
     double T_i;
@@ -1535,14 +1543,16 @@ void k_iter_persist(IterParams<R, VT> P, int n_iter)
     pbar_exit(bar, nblk);
 }
 
-// Before every persistent launch: the state it starts from (the current
-// ping-pong buffer and Ctl), unless a launch has already failed -- then the
-// snapshot of the failed launch's start is kept for the host to restore.
+// Before every persistent / dataflow launch: the state it starts from (the
+// current ping-pong buffer and Ctl), unless a launch has already failed or
+// the run has stopped -- then the snapshot of the failed (or stopping)
+// launch's start is kept for the host to restore (persist_recover,
+// ovr_recover).
 template <typename R>
 __global__ __launch_bounds__(256) void k_persist_snap(const Ctl *ctl, const unsigned *bar, const R *st0, const R *st1,
                                                       R *snap, Ctl *snap_ctl, int64_t n)
 {
-    if (__hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    if (__hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || ctl->stop) return;
     const R *cur = (ctl->done & 1) ? st1 : st0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         snap[i] = cur[i];
@@ -1578,27 +1588,48 @@ __global__ __launch_bounds__(256) void k_persist_snap(const Ctl *ctl, const unsi
 // snapshot and goes on with one launch per iteration (persist_recover).
 //
 // Totals: each tile adds its exact sums into the accumulator slot of its
-// iteration (j & 1); the tile arriving last for iteration j waits for
+// iteration (j % GQ_FLOW_LAG); the tile arriving last for iteration j waits for
 // finalize(j - 1), then reduces the slot and runs fin_apply (acquire and
 // release fences around it: the previous finalizer may have run on another
 // XCD) and publishes the finalized count.  The stop rule: finalize(s) stores
-// 1 + s in the stop word before it publishes; items of iteration >= s + 2
-// see it (they wait for finalize(s)) and leave; iteration s + 1 may already
+// 1 + s in the stop word before it publishes; items of iteration >= s + 1
+// that see it leave, and those of iteration >= s + 2 see it (they wait for
+// finalize(s)); iteration s + 1 may already
 // have run -- it wrote the buffer of state s - 1 -- and its finalize is
 // skipped, so Ctl and the buffer holding state s stay as the whole-grid run
 // leaves them.  State moves between workgroups through device-coherent
 // (agent-scope) loads and stores (ld_state / st_state).
 // ---------------------------------------------------------------------------
+// GQ_FLOW_LAG: iterations an item may run ahead of the finalize -- item j
+// starts once iterations up to j - GQ_FLOW_LAG are finalized.  2 (kept): the
+// buffer an item writes never holds a state that may have met the stop
+// rule.  Deeper (a diagnostic): an item of iteration s + 2 may overwrite the
+// buffer of a state s that met it; the launch then records the overshoot
+// (Ctl::ovr) and the host restores the chunk's snapshot and re-runs up to s
+// with one launch per iteration (ovr_recover).  The timeline of the lag-2
+// form shows items waiting 24% of their time; lags 4, 6 and 8 left both the
+// wait (lag 6: 24%) and C2 / the C3 levels unchanged within 1%
+// (profiles/r06_flow_lag_ab.txt, r06_flow_timeline_lag{2,6}.txt): the wait
+// is the neighbour dependencies -- a band of 116 tiles per XCD against 96
+// resident slots leaves about 1.2 item-times between an item's claim and
+// its neighbours' claims of the previous iteration -- not the finalize.
+#ifndef GQ_FLOW_LAG
+#define GQ_FLOW_LAG 2
+#endif
+constexpr int FL_SLOTS = GQ_FLOW_LAG;              // accumulator / ticket slots (iteration j: j % FL_SLOTS)
 constexpr int FL_LINE = 32;                        // 32-bit words per 128-byte line
 constexpr int FL_Q = 0;                            // 8 per-XCD claim counters, a line each
 constexpr int FL_FIN = 8 * FL_LINE;                // iterations finalized (launch-local)
 constexpr int FL_STOP = 9 * FL_LINE;               // 1 + the launch-local iteration that stopped the run
 constexpr int FL_EXIT = 10 * FL_LINE;              // workgroups that have left
-constexpr int FL_ARR = 11 * FL_LINE;               // arrival tickets of slots 0, 1 (a line each)
-constexpr int FL_ACC = 13 * FL_LINE;               // 2 slots of ACC_SLICES x (NFIX + LMAX) x 4 u64 limbs
+constexpr int FL_MAXJ = 11 * FL_LINE;              // 1 + the largest iteration an item started
+constexpr int FL_ARR = 12 * FL_LINE;               // arrival tickets of the slots (a line each)
+constexpr int FL_ACC = FL_ARR + FL_SLOTS * FL_LINE;  // the slots' ACC_SLICES x (NFIX + LMAX) x 4 u64 limbs
 constexpr int FL_ACC_SLOT = ACC_SLICES * (NFIX + GQMAP_LMAX) * 4;  // u64 per slot
-constexpr int FL_DONE = FL_ACC + 2 * 2 * FL_ACC_SLOT;              // per tile: iterations done (launch-local)
+constexpr int FL_DONE = FL_ACC + 2 * FL_SLOTS * FL_ACC_SLOT;       // per tile: iterations done (launch-local)
 constexpr int flow_words(int ntiles) { return FL_DONE + ntiles; }
+static_assert(FL_SLOTS >= 2, "the finalize lag is at least 2");
+static_assert((FL_ACC & 1) == 0, "u64 alignment of the accumulator slots");
 
 // Wait (wave 0 polls, the workgroup follows) until item (j, tile) may run.
 // Returns 1: run it; 0: leave (the run stopped before iteration j - 1, or a
@@ -1628,9 +1659,9 @@ __device__ __forceinline__ int flow_wait(unsigned *fl, unsigned *bar, int tiles_
             bool ok = true, leave = false;
             if (dep >= 0) ok = __hip_atomic_load(fl + FL_DONE + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)j;
             else if (x == 5 && fin_need > 0) ok = __hip_atomic_load(fl + FL_FIN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)fin_need;
-            else if (x == 6) {
+            else if (x == 6) {  // the run stopped at an earlier iteration (st - 1 < j)
                 const unsigned st = __hip_atomic_load(fl + FL_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                leave = st != 0 && (int)st - 1 <= j - 2;
+                leave = st != 0 && (int)st - 1 < j;
             } else if (x == 7) {
                 leave = __hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             } else if (x == 8) {  // injected failure (tests): at the first item of iteration j
@@ -1669,6 +1700,7 @@ __device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, u
             __builtin_amdgcn_s_sleep(GQ_PERSIST_SLEEP);
         }
         // a run stopped at an earlier iteration: Ctl keeps that iteration
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the stop word is stored before FL_FIN)
         if (go && __hip_atomic_load(fl + FL_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) go = 2;
         *shf = go;
     }
@@ -1685,13 +1717,24 @@ __device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, u
         }
     }
     if (threadIdx.x == 0) {
-        __hip_atomic_store(fl + FL_ARR + (j & 1) * FL_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fl + FL_ARR + (j % FL_SLOTS) * FL_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(fl + FL_FIN, (unsigned)(j + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 // snap: Ctl as the launch found it (k_persist_snap, launched just before):
 // a workgroup dispatched late must not read Ctl after a finalize changed it.
+// GQ_FLOW_TL (diagnostic builds): per item (j, tile) of a launch that starts
+// at iteration 1, four words at (j * items + tile) -- the claim, the end of the dependency wait,
+// the end of the item, and (XCC_ID << 32 | HW_ID) -- read back with
+// gqmap_debug_flow_timeline (scripts/flow_timeline.py).
+#ifndef GQ_FLOW_TL
+#define GQ_FLOW_TL 0
+#endif
+#if GQ_FLOW_TL
+constexpr int FLOW_TL_WORDS = 1 << 18;
+__device__ unsigned long long g_flow_tl[FLOW_TL_WORDS];
+#endif
 #ifndef GQ_FLOW_WAVES  // waves per SIMD the allocation must allow (3: <= 168 VGPRs, as k_iter on C2)
 #define GQ_FLOW_WAVES 3
 #endif
@@ -1723,8 +1766,10 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
     static_assert(!LIT || (ENG == 0 && Q == 1), "literal order: the mixture engine at one lane per node");
     unsigned *bar = P.bar;
     // a stopped run, or a failed launch earlier in the replay (whose
-    // snapshot the host restores): nothing to do but take the exit ticket
-    const bool run = !snap->stop &&
+    // snapshot the host restores): nothing to do but take the exit ticket.
+    // (Ctl's own stop word too: after a stop the snapshot is not refreshed;
+    // within this launch it only turns to 1 once the run has stopped.)
+    const bool run = !snap->stop && __hip_atomic_load(&P.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
                      __hip_atomic_load(bar + BAR_FAIL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
     const int it0 = snap->it, done0 = snap->done;
     const double T0 = snap->T;
@@ -1768,12 +1813,20 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
         const int it = it0 + j, parity = (done0 + j) & 1;
         // finalize(j - 1) changed alpha (fin_apply: it - 1 > alpha_start, L > 1)
         const bool alpha_moved = P.L > 1 && it - 1 > P.fin.alpha_start;
-        if (!flow_wait(fl, bar, P.tiles_m, ntiles, tile, l, L, j, alpha_moved ? j : j - 1, &sh_go)) break;
+#if GQ_FLOW_TL
+        const unsigned long long tl_claim = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (!flow_wait(fl, bar, P.tiles_m, ntiles, tile, l, L, j, alpha_moved ? j : j - GQ_FLOW_LAG + 1, &sh_go)) break;
+        if (GQ_FLOW_LAG > 2 && threadIdx.x == 0)  // (for the overshoot check at the exit)
+            __hip_atomic_fetch_max(fl + FL_MAXJ, (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if GQ_FLOW_TL
+        const unsigned long long tl_go = __builtin_amdgcn_s_memrealtime();
+#endif
         double T = T0;  // fin_apply's temperature decay after each earlier iteration
         if (P.fin.t_decay_every > 0)
             for (int q = it0; q < it; ++q)
                 if (q % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
-        unsigned long long *slot = acc + (size_t)(j & 1) * FL_ACC_SLOT;
+        unsigned long long *slot = acc + (size_t)(j % FL_SLOTS) * FL_ACC_SLOT;
         const int l0 = ENG == 1 ? l : 0, l1 = ENG == 1 ? l + 1 : 1;  // (L = 1 unless super)
         if (GQ_FLOW_MIX && ENG == 0 && !LIT && edge_first)
             iter_tile<R, VT, ENG, Q, true, GQ_FLOW_COH, false, LIT>(P, tile, it, parity, 0, lds, l0, l1, T, false, slot);
@@ -1782,9 +1835,20 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
         // publish: every wave's stores (state, rou, the slot's sums) are done
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#if GQ_FLOW_TL
+        const size_t tli = (size_t)j * nitems + (size_t)tile * L + l;  // (iteration, tile, component)
+        if (threadIdx.x == 0 && (tli + 1) * 4 <= (size_t)FLOW_TL_WORDS && snap->it == 1) {
+            unsigned long long *w = g_flow_tl + tli * 4;
+            w[0] = tl_claim;
+            w[1] = tl_go;
+            w[2] = __builtin_amdgcn_s_memrealtime();
+            w[3] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                   (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        }
+#endif
         if (threadIdx.x == 0) {
             __hip_atomic_store(fl + FL_DONE + tile * L + l, (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned tk = __hip_atomic_fetch_add(fl + FL_ARR + (j & 1) * FL_LINE, 1u, __ATOMIC_RELAXED,
+            const unsigned tk = __hip_atomic_fetch_add(fl + FL_ARR + (j % FL_SLOTS) * FL_LINE, 1u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT);
             if (GQ_FLOW_PAIR) sh_i = (int)__hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sh_last = tk == (unsigned)(nitems - 1);
@@ -1800,6 +1864,14 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
         sh_last = __hip_atomic_fetch_add(fl + FL_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (sh_last) {
+        if (threadIdx.x == 0 && GQ_FLOW_LAG > 2) {
+            // an item of iteration >= s + 2 ran after the stop at s: the
+            // buffer of state s may be overwritten -- the host recovers
+            const unsigned st = __hip_atomic_load(fl + FL_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned mj = __hip_atomic_load(fl + FL_MAXJ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st != 0 && mj >= st + 2) __hip_atomic_store(&P.ctl->ovr, (int)st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
         for (int w = threadIdx.x; w < flow_words(nitems); w += blockDim.x)
             __hip_atomic_store(fl + w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1838,7 +1910,7 @@ __global__ __launch_bounds__(256) void k_seq_snap(const Ctl *ctl, const R *st0, 
 // iteration order and applied with fin_apply -- the trace, it / done / T and
 // the stop rule exactly as the whole grid's finalize.  A stop met before the
 // last row means the sequence's later iterations have already run: Ctl::ovr
-// = row + 1 tells the host to recover (deferred_recover).  One workgroup.
+// = row + 1 tells the host to recover (ovr_recover).  One workgroup.
 __global__ __launch_bounds__(256) void k_finalize_seq(FinParams F, const fix128 *rows, int n)
 {
     Ctl *ctl = F.ctl;
@@ -3032,7 +3104,7 @@ gqmap_status launch_step_rccl(gqmap_ctx *c, hipEvent_t e0 = nullptr, hipEvent_t 
 // i + 1 .. n - 1 have already run: k_finalize_seq records Ctl::ovr = i + 1,
 // later sequences turn into no-ops (Ctl::stop), and the host restores the
 // snapshot and re-runs the i + 1 iterations with the exact per-iteration
-// step (deferred_recover) -- the same state, trace and stop iteration as the
+// step (ovr_recover) -- the same state, trace and stop iteration as the
 // whole grid.
 // (the snapshot buffers are allocated outside any capture -- gqmap_tile_attach_rccl,
 // capture_steps -- and follow the grid size; without them the exact step runs)
@@ -3113,24 +3185,27 @@ gqmap_status launch_seq_deferred(gqmap_ctx *c, int n, hipEvent_t *ev = nullptr)
     return GQMAP_OK;
 }
 
-// After a run: a deferred sequence overshot its stop iteration (Ctl::ovr):
-// restore the sequence's snapshot (state + Ctl at its start) and re-run its
+gqmap_status launch_step(gqmap_ctx *c);
+
+// After a run: a deferred sequence, or a dataflow launch deeper than lag 2
+// (GQ_FLOW_LAG), overshot its stop iteration (Ctl::ovr): restore the
+// sequence's / launch's snapshot (state + Ctl at its start) and re-run its
 // first ovr iterations with the exact per-iteration step, which stops at the
 // same iteration as the whole grid.  Every rank sees the same all-gathered
 // totals, so every rank recovers together (the re-run's collectives match).
-gqmap_status deferred_recover(gqmap_ctx *c, const Ctl &h, bool *recovered)
+gqmap_status ovr_recover(gqmap_ctx *c, const Ctl &h, bool *recovered)
 {
     *recovered = false;
-    if (!deferred(c) || h.ovr == 0) return GQMAP_OK;
+    if (h.ovr == 0 || !c->d_snap) return GQMAP_OK;
     c->ctl_known = false;
     Ctl snap;
     GQ_HIP(hipMemcpyAsync(&snap, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
     GQ_HIP(hipStreamSynchronize(c->stream));
-    GQ_HIP(hipMemcpyAsync(c->d_st[snap.done & 1], c->d_snap, (size_t)c->MNL * NPLANES * c->rsz, hipMemcpyDeviceToDevice,
-                          c->stream));
+    GQ_HIP(hipMemcpyAsync(c->d_st[snap.done & 1], c->d_snap, c->snap_bytes, hipMemcpyDeviceToDevice, c->stream));
     GQ_HIP(hipMemcpyAsync(c->d_ctl, c->d_snap_ctl, sizeof(Ctl), hipMemcpyDeviceToDevice, c->stream));
+    if (c->d_flow) GQ_HIP(hipMemsetAsync(c->d_flow, 0, sizeof(unsigned) * c->flow_n, c->stream));
     for (int i = 0; i < h.ovr; ++i) {
-        gqmap_status st = launch_step_rccl(c);
+        gqmap_status st = launch_step(c);
         if (st != GQMAP_OK) return st;
     }
     GQ_HIP(hipStreamSynchronize(c->stream));
@@ -3978,9 +4053,9 @@ gqmap_status gqmap_run_aepe(gqmap_ctx *c, int n_iter, int *n_done, double *trace
             if ((s = persist_recover(c, &recovered)) != GQMAP_OK) return s;
             if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
         }
-        if (h.ovr) {  // a deferred RCCL sequence ran past its stop iteration
+        if (h.ovr) {  // a deferred RCCL sequence / deep dataflow launch ran past its stop iteration
             bool again = false;
-            if ((s = deferred_recover(c, h, &again)) != GQMAP_OK) return s;
+            if ((s = ovr_recover(c, h, &again)) != GQMAP_OK) return s;
             if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
             // (the finalize had already recorded the trace up to the stop; the
             // exact re-run rewrote the same slots -- read them again anyway)
@@ -4057,7 +4132,7 @@ gqmap_status gqmap_run_timed(gqmap_ctx *c, int n_iter, int *n_done, double *tota
     if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
     if (h.ovr) {
         bool again = false;
-        if ((s = deferred_recover(c, h, &again)) != GQMAP_OK) return s;
+        if ((s = ovr_recover(c, h, &again)) != GQMAP_OK) return s;
         if ((s = read_ctl(c, &h)) != GQMAP_OK) return s;
     }
     if (c->d_snap && !c->comm) {  // a failed persistent / dataflow launch: restored, finished per launch
@@ -4138,6 +4213,22 @@ gqmap_status gqmap_debug_persist_fault(gqmap_ctx *c, int j)
 // Not in the public header (tests): 1 when the context has fallen back from
 // the persistent launch to one launch per iteration.
 int gqmap_debug_persist_off(const gqmap_ctx *c) { return c && c->persist_off ? 1 : 0; }
+
+// Not in the public header (diagnostic builds with GQ_FLOW_TL): the flow
+// timeline words (item (j, tile) at 4 (j * tiles + tile)); returns the
+// words copied, or -1 in a build without it.
+int gqmap_debug_flow_timeline(unsigned long long *out, int n)
+{
+#if GQ_FLOW_TL
+    n = std::min(n, FLOW_TL_WORDS);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_flow_tl), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    return n;
+#else
+    (void)out;
+    (void)n;
+    return -1;
+#endif
+}
 
 // Not in the public header (bench, tests): 1 when the context's runs take
 // the dataflow launch (k_iter_flow) -- allocates its queue buffer if needed.

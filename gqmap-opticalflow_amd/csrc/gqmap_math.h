@@ -969,13 +969,56 @@ inline void lit_table_point(double *row8, double xi, double xj, double wi, doubl
 #ifndef GQ_LIT_CSE
 #define GQ_LIT_CSE (GQ_LIT_FORM >= 2)
 #endif
+// fmin / fmax of non-NaN operands (the clamp's): on the device the bare
+// v_min_f64 / v_max_f64.  Through fmin the compiler re-canonicalises the
+// loop-invariant bound (a v_max_f64 x, x) at every quadrature point -- 4 of
+// the node loop's ~174 VALU instructions.  The same IEEE result: min / max of
+// two numbers is exact, and a NaN operand gives the other one either way.
+GQ_HD double lit_min(double a, double b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmin(a, b);
+#endif
+}
+GQ_HD double lit_max(double a, double b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmax(a, b);
+#endif
+}
+#ifndef GQ_LIT_ASM_MINMAX
+#define GQ_LIT_ASM_MINMAX 1
+#endif
+#if GQ_LIT_ASM_MINMAX
+#define GQ_LMIN lit_min
+#define GQ_LMAX lit_max
+#else
+#define GQ_LMIN fmin
+#define GQ_LMAX fmax
+#endif
+// GQ_LIT_ADDR: the four tap columns as one cell offset plus multiples of the
+// column stride (byte offsets, as bicubic_w4) instead of a multiply each.
+// With GQ_LIT_ASM_MINMAX: 174 -> 165 VALU instructions per node-gradient
+// point, k_iter_lit 271.8 -> 268.1 us, graph 255.0 -> 250.4 us per iteration,
+// the same checksum (profiles/r06_lit_minmax_addr_ab.txt).
+#ifndef GQ_LIT_ADDR
+#define GQ_LIT_ADDR 1
+#endif
 template <typename VP>
 GQ_HD double lit_interp(VP VV, int M2, int Mo, int No, double Xq, double Yq)
 {
-    Xq = fmin(fmax(Xq, 1.0), (double)No);
-    Yq = fmin(fmax(Yq, 1.0), (double)Mo);
+    Xq = GQ_LMIN(GQ_LMAX(Xq, 1.0), (double)No);
+    Yq = GQ_LMIN(GQ_LMAX(Yq, 1.0), (double)Mo);
 #if GQ_LIT_CELL
-    const double fx = fmin(floor(Xq), (double)(No - 1)), fy = fmin(floor(Yq), (double)(Mo - 1));
+    const double fx = GQ_LMIN(floor(Xq), (double)(No - 1)), fy = GQ_LMIN(floor(Yq), (double)(Mo - 1));
     const int ix = (int)fx, iy = (int)fy;
     const double so = Xq - fx, to = Yq - fy;
 #else
@@ -992,10 +1035,19 @@ GQ_HD double lit_interp(VP VV, int M2, int Mo, int No, double Xq, double Yq)
     const double t1 = (3.0 * to - 5.0) * to * to + 2.0;
     const double t2 = ((4.0 - 3.0 * to) * to + 1.0) * to;
     const double t3 = (to - 1.0) * to * to;
+#if GQ_LIT_ADDR
+    constexpr uint32_t E = (uint32_t)sizeof(*VV);
+    const uint32_t ob = cell_elem(iy, ix, M2) * E, cb = (uint32_t)M2 * E;
+    const auto c1 = byte_ptr(VV, ob);
+    const auto c2 = byte_ptr(VV, ob + cb);
+    const auto c3 = byte_ptr(VV, ob + 2 * cb);
+    const auto c4 = byte_ptr(VV, ob + 3 * cb);
+#else
     const auto c1 = elem_ptr(VV, cell_elem(iy, ix, M2));
     const auto c2 = elem_ptr(VV, cell_elem(iy, ix + 1, M2));
     const auto c3 = elem_ptr(VV, cell_elem(iy, ix + 2, M2));
     const auto c4 = elem_ptr(VV, cell_elem(iy, ix + 3, M2));
+#endif
     double ss = ((2.0 - so) * so - 1.0) * so;
     double Vq = (((double)c1[0] * ss * t0 + (double)c1[1] * ss * t1) + (double)c1[2] * ss * t2) +
                 (double)c1[3] * ss * t3;
@@ -1180,6 +1232,32 @@ GQ_HD void lit_points_mirror(TP tab, const LitCoef &c, double p, LitAcc &S, PT p
     }
 }
 
+// The node gradient's loop at K = 9 with the rows unrolled GQ_LIT_NODE_UNROLL
+// times (1: the runtime-K loop): the next point's tap gathers can then issue
+// before this point's taps are summed.  The same operations in the same order.
+// Measured 2 / 3: 297.8 / 298.2 against 268.1 us (register pressure at the
+// 3-wave bound; profiles/r06_lit_minmax_addr_ab.txt): not used.
+#ifndef GQ_LIT_NODE_UNROLL
+#define GQ_LIT_NODE_UNROLL 1
+#endif
+template <int KK, typename TP, typename PT>
+GQ_HD void lit_points_fixed(TP tab, const LitCoef &c, double p, LitAcc &S, PT pt)
+{
+    for (int cc = 0, k0 = 0; cc < KK; ++cc, k0 += KK) {
+        const double XI = tab[tab_at(TL_XI, k0)];
+        const double sXI = c.s * XI, tXI = c.t * XI;
+#ifdef __HIPCC__
+#pragma unroll GQ_LIT_NODE_UNROLL
+#endif
+        for (int r = 0; r < KK; ++r) {
+            const int k = k0 + r;
+            const double XJ = tab[tab_at(TL_XJ, k)];
+            const double zi = sXI + c.t * XJ, zj = tXI + c.s * XJ;
+            S.add(tab, k, pt(k, zi, zj), zi, zj, p, c.sqrtpr, c.rsqrtpr, true);
+        }
+    }
+}
+
 template <typename TP, typename PT>
 GQ_HD void lit_points_dyn(TP tab, int K2, const LitCoef &c, double p, LitAcc &S, PT pt, bool live)
 {
@@ -1233,6 +1311,9 @@ GQ_HD Grad<double> lit_node_grad(TP tab, int K2, VP VV, int M2, IP I1, int Mo, i
     };
 #if GQ_LIT_MIRROR && GQ_LIT_MIRROR_NODE
     if (K2 == 81 && live) lit_points_mirror<9>(tab, c, p, S, pt);
+    else
+#elif GQ_LIT_NODE_UNROLL > 1
+    if (K2 == 81 && live) lit_points_fixed<9>(tab, c, p, S, pt);
     else
 #endif
         lit_loop(tab, K2, c, p, live, S, pt);
