@@ -1128,26 +1128,44 @@ GQ_HD LitCoef lit_coef(double p)
 }
 
 // Epilogues: node (:107-115, entropy -3T) and edge (:137-145, entropy +T).
+// GQ_LIT_PIDIV: the six divisions by pi as div_rcp with RN(1/pi) (5
+// operations instead of the general division's ~10; the same correctly
+// rounded quotient -- div_rcp's conditions hold: pi's reciprocal rounded
+// once, sums far from overflow and underflow).  Bit-identical over
+// tests/test_gpu_literal.py, but neutral (264.9 vs 263.7 us, 30 of ~32k
+// instructions per node-lane; profiles/r06_lit_xj_pidiv_ab.txt): off.
+#ifndef GQ_LIT_PIDIV
+#define GQ_LIT_PIDIV 0
+#endif
+GQ_HD double lit_div_pi(double x)
+{
+#if GQ_LIT_PIDIV
+    constexpr double rpi = 1.0 / GQ_M_PI;
+    return div_rcp(x, GQ_M_PI, rpi);
+#else
+    return x / GQ_M_PI;
+#endif
+}
 GQ_HD Grad<double> lit_epi(const LitAcc &S, const LitCoef &c, double a, double o1, double o2, double p, double T,
                            bool node)
 {
     const double o1pr = GQ_M_SQRT2 / (o1 * c.pr), o2pr = GQ_M_SQRT2 / (o2 * c.pr);
     Grad<double> g;
-    g.du1 = a * S.du1 * o1pr / GQ_M_PI;
-    g.du2 = a * S.du2 * o2pr / GQ_M_PI;
+    g.du1 = lit_div_pi(a * S.du1 * o1pr);
+    g.du2 = lit_div_pi(a * S.du2 * o2pr);
     // T (const1 + log(.)): a finite value times 0 when T = 0 -- skipped then
     // (the difference Ei/pi -+ 0 is Ei/pi: Ei < 0 never vanishes)
     const double ent = T != 0 ? (1 + gq_log(2 * GQ_M_PI)) + gq_log(c.sqrtpr * o1 * o2) : 0.0;
     if (node) {
-        g.da = S.Ei / GQ_M_PI - 3 * T * ent;
-        g.do1 = a * (S.do1 / GQ_M_PI - 3 * T) / o1;
-        g.do2 = a * (S.do2 / GQ_M_PI - 3 * T) / o2;
-        g.dp = a * (S.dp / GQ_M_PI + 3 * T * p) / c.pr;
+        g.da = lit_div_pi(S.Ei) - 3 * T * ent;
+        g.do1 = a * (lit_div_pi(S.do1) - 3 * T) / o1;
+        g.do2 = a * (lit_div_pi(S.do2) - 3 * T) / o2;
+        g.dp = a * (lit_div_pi(S.dp) + 3 * T * p) / c.pr;
     } else {
-        g.da = S.Ei / GQ_M_PI + T * ent;
-        g.do1 = a * (S.do1 / GQ_M_PI + T) / o1;
-        g.do2 = a * (S.do2 / GQ_M_PI + T) / o2;
-        g.dp = a * (S.dp / GQ_M_PI - T * p) / c.pr;
+        g.da = lit_div_pi(S.Ei) + T * ent;
+        g.do1 = a * (lit_div_pi(S.do1) + T) / o1;
+        g.do2 = a * (lit_div_pi(S.do2) + T) / o2;
+        g.dp = a * (lit_div_pi(S.dp) - T * p) / c.pr;
     }
     g.E = a * g.da;
     return g;
@@ -1156,16 +1174,31 @@ GQ_HD Grad<double> lit_epi(const LitAcc &S, const LitCoef &c, double a, double o
 // The quadrature loop of a gradient, points k = r + K c in meshgrid order
 // (column c outer, row r inner: the reference's k = 1..K^2): pt(k, zi, zj)
 // returns the point's fval.  Form 2 forms s*XI and t*XI once per column.
+// GQ_LIT_XJ_PREFETCH: the next point's XJ (a scalar load) issued during
+// this point, so a point does not start with a wait on the scalar cache.
+// Measured 263.7 -> 298.3 us (the node loop's schedule falls apart, as with
+// GQ_LIT_NODE_UNROLL; profiles/r06_lit_xj_pidiv_ab.txt): off.
+#ifndef GQ_LIT_XJ_PREFETCH
+#define GQ_LIT_XJ_PREFETCH 0
+#endif
 template <bool LIVE, typename TP, typename PT>
 GQ_HD void lit_points(TP tab, int K2, const LitCoef &c, double p, LitAcc &S, PT pt)
 {
 #if GQ_LIT_CSE
     const int K = lit_k(K2);
+#if GQ_LIT_XJ_PREFETCH
+    double XJn = tab[tab_at(TL_XJ, 0)];
+#endif
     for (int cc = 0, k = 0; cc < K; ++cc) {
         const double XI = tab[tab_at(TL_XI, k)];
         const double sXI = c.s * XI, tXI = c.t * XI;
         for (int r = 0; r < K; ++r, ++k) {
+#if GQ_LIT_XJ_PREFETCH
+            const double XJ = XJn;
+            XJn = tab[tab_at(TL_XJ, k + 1 < K2 ? k + 1 : k)];
+#else
             const double XJ = tab[tab_at(TL_XJ, k)];
+#endif
             const double zi = sXI + c.t * XJ, zj = tXI + c.s * XJ;
             S.add(tab, k, pt(k, zi, zj), zi, zj, p, c.sqrtpr, c.rsqrtpr, LIVE);
         }
