@@ -1735,8 +1735,17 @@ __device__ void flow_finalize(const FinParams &F, unsigned *fl, unsigned *bar, u
 constexpr int FLOW_TL_WORDS = 1 << 18;
 __device__ unsigned long long g_flow_tl[FLOW_TL_WORDS];
 #endif
-#ifndef GQ_FLOW_WAVES  // waves per SIMD the allocation must allow (3: <= 168 VGPRs, as k_iter on C2)
-#define GQ_FLOW_WAVES 3
+// Waves per SIMD the allocation must allow at one lane per node.  2 (<= 256
+// VGPRs): the C2 fp64 kernel takes 215 and spills nothing (at 3, as k_iter
+// on C2: 167 + 144 bytes of scratch), and the 512 resident slots leave a band
+// of 116 tiles ~64 items in flight -- more slack for the neighbour
+// dependencies; C2 fp64 142.9 -> 139.6 us/it (graph), the 480x640 ctf level
+// ~278 -> ~275 (profiles/r06_flow_2waves_ab.txt, same checksums).
+#ifndef GQ_FLOW_WAVES
+#define GQ_FLOW_WAVES 2
+#endif
+#ifndef GQ_FLOW_LIT_WAVES  // the same for the literal-order instantiation (2: <= 256 VGPRs, no spills)
+#define GQ_FLOW_LIT_WAVES 2
 #endif
 #ifndef GQ_FLOW_MIX  // node-first / edge-first alternation among co-resident workgroups
 #define GQ_FLOW_MIX 1
@@ -1759,7 +1768,7 @@ __device__ unsigned long long g_flow_tl[FLOW_TL_WORDS];
 #define GQ_FLOW_ROWS 1
 #endif
 template <typename R, typename VT, int ENG, int Q, bool LIT = false>
-__global__ __launch_bounds__(BLOCK, Q == 1 ? GQ_FLOW_WAVES : ENG == 1 ? 2 : min_waves(ENG, Q))
+__global__ __launch_bounds__(BLOCK, LIT ? GQ_FLOW_LIT_WAVES : Q == 1 ? GQ_FLOW_WAVES : ENG == 1 ? 2 : min_waves(ENG, Q))
 void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, const Ctl *snap)
 {
     static_assert(Q >= 1 && Q <= 4, "1..4 lanes per node");
@@ -3297,10 +3306,13 @@ bool launch_flow_t(gqmap_ctx *c, int n, bool dry)
     if (c->opt.engine != GQMAP_ENGINE_CTF) {
         if constexpr (sizeof(R) == 8 && sizeof(VT) == 4) {
             // the literal-order arithmetic on integer frames (C2's parity-carrying
-            // engine): bit-exact as items, but its kernel sits at 167 VGPRs and
-            // the dataflow wrapper spills 20 (274.7 -> 283 us/it,
-            // profiles/r06_lit_flow_ab.txt): only when forced
-            if (c->lit) return c->pol.flow > 0 && c->kq == 1 && launch_flow_q<R, VT, 0, 1, true>(c, n, dry);
+            // engine), bit-exact as items.  At the per-launch kernel's 3 waves
+            // per SIMD the dataflow wrapper spills (224 bytes; 251 -> 265 us/it,
+            // profiles/r06_lit_flow_ab2.txt); allowed 2 waves (GQ_FLOW_LIT_WAVES:
+            // 243 VGPRs, no scratch, 512 slots -- a band of 116 tiles then has
+            // ~64 items in flight, more slack for the neighbour dependencies)
+            // it runs 250.8 -> 224.5 us/it (profiles/r06_lit_flow_2waves_ab.txt)
+            if (c->lit) return c->pol.flow != 0 && c->kq == 1 && launch_flow_q<R, VT, 0, 1, true>(c, n, dry);
         }
         return !c->lit && c->kq == 1 && launch_flow_q<R, VT, 0, 1>(c, n, dry);
     }
