@@ -1750,6 +1750,9 @@ __device__ unsigned long long g_flow_tl[FLOW_TL_WORDS];
 #ifndef GQ_FLOW_MIX  // node-first / edge-first alternation among co-resident workgroups
 #define GQ_FLOW_MIX 1
 #endif
+#ifndef GQ_FLOW_LIT_MIX
+#define GQ_FLOW_LIT_MIX 0
+#endif
 #ifndef GQ_FLOW_COH  // device-coherent state access (0: plain -- timing experiments only, not coherent)
 #define GQ_FLOW_COH 1
 #endif
@@ -1767,8 +1770,10 @@ __device__ unsigned long long g_flow_tl[FLOW_TL_WORDS];
 #ifndef GQ_FLOW_ROWS
 #define GQ_FLOW_ROWS 1
 #endif
-template <typename R, typename VT, int ENG, int Q, bool LIT = false>
-__global__ __launch_bounds__(BLOCK, LIT ? GQ_FLOW_LIT_WAVES : Q == 1 ? GQ_FLOW_WAVES : ENG == 1 ? 2 : min_waves(ENG, Q))
+// W > 0: the waves per SIMD, overriding the defaults above (the large-frame
+// instantiation, launch_flow_q)
+template <typename R, typename VT, int ENG, int Q, bool LIT = false, int W = 0>
+__global__ __launch_bounds__(BLOCK, W > 0 ? W : LIT ? GQ_FLOW_LIT_WAVES : Q == 1 ? GQ_FLOW_WAVES : ENG == 1 ? 2 : min_waves(ENG, Q))
 void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, const Ctl *snap)
 {
     static_assert(Q >= 1 && Q <= 4, "1..4 lanes per node");
@@ -1791,9 +1796,10 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
     // in the queue), one otherwise (L = 1)
     const int L = ENG == 1 ? P.L : 1, nbl = nb * L, nitems = ntiles * L;
     constexpr int INV = ENG == 2 && Q == 1 ? GQ_PHASE_MIX_CTF_Q1_INV : GQ_PHASE_MIX_OTHER_INV;
-    // (the phase mix: the fast mixture engine only -- the literal kernel's
-    // second instantiation would spill)
-    const bool edge_first = GQ_FLOW_MIX && ENG == 0 && !LIT && ((((b >> 3) / P.cu_slots) & 1) != INV);
+    // (the phase mix: the fast mixture engine; the literal kernel's with
+    // GQ_FLOW_LIT_MIX -- its second instantiation spilled at 3 waves)
+    constexpr bool MIX = GQ_FLOW_MIX && ENG == 0 && (!LIT || GQ_FLOW_LIT_MIX);
+    const bool edge_first = MIX && ((((b >> 3) / P.cu_slots) & 1) != INV);
     __shared__ TileLdsQ<R, Q> lds;
     __shared__ int sh_i, sh_go, sh_last;
     __shared__ double tot[NFIX + GQMAP_LMAX];
@@ -1837,7 +1843,7 @@ void k_iter_flow(IterParams<R, VT> P, int n_iter, unsigned *fl, int ntiles, cons
                 if (q % P.fin.t_decay_every == 0) T = fmax(T * P.fin.drate, P.fin.t_min);
         unsigned long long *slot = acc + (size_t)(j % FL_SLOTS) * FL_ACC_SLOT;
         const int l0 = ENG == 1 ? l : 0, l1 = ENG == 1 ? l + 1 : 1;  // (L = 1 unless super)
-        if (GQ_FLOW_MIX && ENG == 0 && !LIT && edge_first)
+        if (MIX && edge_first)
             iter_tile<R, VT, ENG, Q, true, GQ_FLOW_COH, false, LIT>(P, tile, it, parity, 0, lds, l0, l1, T, false, slot);
         else
             iter_tile<R, VT, ENG, Q, false, GQ_FLOW_COH, false, LIT>(P, tile, it, parity, 0, lds, l0, l1, T, false, slot);
@@ -3250,6 +3256,20 @@ gqmap_status launch_steps(gqmap_ctx *c, int n)
 void drop_graph(gqmap_ctx *c);
 
 // ---- dataflow launch (k_iter_flow, policy flow) ---------------------------
+#ifndef GQ_FLOW_WIDE_ITEMS  // items per iteration above which the 3-wave form runs
+#define GQ_FLOW_WIDE_ITEMS 4096
+#endif
+template <typename R, typename VT, int ENG, int Q, bool LIT, int W>
+void flow_launch(gqmap_ctx *c, IterParams<R, VT> P, int n, int nitems, int ntiles)
+{
+    static const int2 shape = kernel_shape(k_iter_flow<R, VT, ENG, Q, LIT, W>);
+    P.cu_group = 1;
+    P.cu_slots = std::max(1, shape.y / 8);
+    // one workgroup per resident slot (more would only queue behind them)
+    const int G = std::max(8, std::min(shape.x * shape.y, nitems));
+    k_iter_flow<R, VT, ENG, Q, LIT, W><<<G, BLOCK, 0, c->stream>>>(P, n, c->d_flow, ntiles, c->d_snap_ctl);
+}
+
 template <typename R, typename VT, int ENG, int Q, bool LIT = false>
 bool launch_flow_q(gqmap_ctx *c, int n, bool dry)
 {
@@ -3280,12 +3300,16 @@ bool launch_flow_q(gqmap_ctx *c, int n, bool dry)
                                                        (const R *)c->d_st[1], (R *)c->d_snap, c->d_snap_ctl, nv);
     }
     IterParams<R, VT> P = iter_params<R, VT>(c);
-    static const int2 shape = kernel_shape(k_iter_flow<R, VT, ENG, Q, LIT>);
-    P.cu_group = 1;
-    P.cu_slots = std::max(1, shape.y / 8);
-    // one workgroup per resident slot (more would only queue behind them)
-    const int G = std::max(8, std::min(shape.x * shape.y, nitems));
-    k_iter_flow<R, VT, ENG, Q, LIT><<<G, BLOCK, 0, c->stream>>>(P, n, c->d_flow, ntiles, c->d_snap_ctl);
+    if constexpr (ENG == 0 && Q == 1 && !LIT) {
+        // a large frame (C5: ~14k tiles) has slack enough at any occupancy and
+        // wants the latency hiding of 3 waves per SIMD: 2 waves measured
+        // 2551 -> 2726 us per iteration on C5
+        if (nitems > GQ_FLOW_WIDE_ITEMS) {
+            flow_launch<R, VT, ENG, Q, LIT, 3>(c, P, n, nitems, ntiles);
+            return true;
+        }
+    }
+    flow_launch<R, VT, ENG, Q, LIT, 0>(c, P, n, nitems, ntiles);
     return true;
 }
 

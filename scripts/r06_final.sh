@@ -21,7 +21,7 @@ if [ "$STEP" = main ] || [ "$STEP" = bench ]; then
   echo "bench ok"
 fi
 if [ "$STEP" = main ] || [ "$STEP" = profile ]; then
-  TAG=r06 timeout -k 10 900 bash scripts/r06_profile_c2.sh || exit $?
+  TAG=${TAG:-r06} timeout -k 10 900 bash scripts/r06_profile_c2.sh || exit $?
 fi
 if [ "$STEP" = configs ]; then
   : > gpurun_out/r06_final_configs.jsonl

@@ -217,3 +217,20 @@ def test_flow_super_mixture_components_bit_exact(alpha_start, its):
     assert d0 == d1 == its
     np.testing.assert_array_equal(t1, t0)
     _same(s1, s0)
+
+
+def test_flow_wide_frame_bit_exact():
+    """A frame beyond GQ_FLOW_WIDE_ITEMS items per iteration (RubberWhale
+    upsampled 3x, 1164 x 1752: 8030 tiles) takes the 3-wave instantiation of
+    the dataflow launch (C5's frames): per-launch trace and state bit for bit
+    over a graph chunk and a leftover."""
+    from gqmap_opticalflow_amd import flow_to_color, flowio
+    I1, I2, gt = flowio.load_pair_scaled("rubberwhale", 3.0)
+    _, _, (minu, maxu, minv, maxv), _ = flow_to_color(gt)
+    o = dict(K=9, L=1, temperature=0.0, drate=0.5, epsn=1e-6, lambdad=1.0, lambdas=5.0,
+             minu=minu, maxu=maxu, minv=minv, maxv=maxv)
+    d0, t0, s0 = _run(o, I1, I2, 61, False)
+    d1, t1, s1 = _run(o, I1, I2, 61, True)
+    assert d0 == d1 == 61
+    np.testing.assert_array_equal(t1, t0)
+    _same(s1, s0)

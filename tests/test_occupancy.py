@@ -40,9 +40,9 @@ LIMITS = {
     "_ZN2gq10k_iter_litIfLb1EEEvNS_10IterParamsIdT_EE": 168,
     # the dataflow launches (k_iter_flow): 2 waves per SIMD, no spills -- C2
     # fp64 fast and literal-order, the C3 480x640 level
-    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE": 256,
-    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb1EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE": 256,
-    "_ZN2gq11k_iter_flowIdfLi2ELi1ELb0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE": 256,
+    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb0ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE": 256,
+    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb1ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE": 256,
+    "_ZN2gq11k_iter_flowIdfLi2ELi1ELb0ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE": 256,
 }
 # kernels that must run without a private (scratch) segment: the C2 kernels
 # of the fast arithmetic; the literal kernel is held to 3 waves by its launch
@@ -52,8 +52,8 @@ LIMITS = {
 NO_SCRATCH = (
     "_ZN2gq6k_iterIdfLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
     "_ZN2gq6k_iterIffLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
-    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE",
-    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb1EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE",
+    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb0ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE",
+    "_ZN2gq11k_iter_flowIdfLi0ELi1ELb1ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE",
 )
 SCRATCH_MAX = {
     "_ZN2gq10k_iter_litIfLb0EEEvNS_10IterParamsIdT_EE": 128,
