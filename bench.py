@@ -519,12 +519,18 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     Mo, No = I1.shape
     ksuf = {"mixture": 0, "super": 1}[engine]
     R = "double" if args.precision == "fp64" else "float"
+    # the padded frame's store (integer frames): binary16 column pairs for
+    # the fp64 mixture engine at one lane per node (policy vv_pair), else float
+    pair = (engine == "mixture" and args.precision == "fp64" and split == 1 and "vv_pair=0" not in args.policy)
+    vvt = "vvh2_t" if pair else "float"
+    vvs = ("VV stored as binary16 column pairs: integer frames" if pair else
+           "VV stored as float: integer frames")
     return dict(elapsed=elapsed, kernel_ms=kernel_ms, instrumented_ms=total_ms, pixels=Mo * No, nodes=nodes, aepe=a, name=name,
                 settle=settle, maps_it=maps_it, literal=lit,
                 I1=I1, I2=I2, opts=opts, Mo=Mo, No=No, map=mpg, gate_its=gate_its, map1=mp1, flo=flo, unk=unk, split=split, seed=rank,
-                kernel=(f"gq::k_iter_flow<{R},float,{ksuf},1> (dataflow launch: one per 50-iteration chunk, the "
-                        f"per-iteration average; VV stored as float)" if dataflow else
-                        f"gq::k_iter<{R},float,{ksuf},Q> (VV stored as float: integer frames)"),
+                kernel=(f"gq::k_iter_flow<{R},{vvt},{ksuf},1> (dataflow launch: one per 50-iteration chunk, the "
+                        f"per-iteration average; {vvs})" if dataflow else
+                        f"gq::k_iter<{R},{vvt},{ksuf},Q> ({vvs})"),
                 dataflow=dataflow,
                 workload=f"{label}: {name} {No}x{Mo} {engine} L={L} K={K} its={args.steps} "
                          f"(one step = one full-frame iteration)")

@@ -2201,6 +2201,7 @@ struct Policy {
     int graph = 1;         // replayed hipGraphs (0: direct launches)
     int flow = -1;         // dataflow launch (k_iter_flow): -1 auto (fp64 whole grids at Q = 1, 2), 0 off, 1 on
     int vv_float = 1;      // float padded-frame store when exact
+    int vv_pair = 1;       // binary16 column-pair store when exact (fp64 single-scale mixture, Q = 1)
     int verbose = 0;       // recovery messages on stderr
 };
 Policy g_pol;
@@ -2240,6 +2241,7 @@ struct gqmap_ctx {
     int tiles_m = 0, tiles_n = 0, nblocks = 0;
     bool have_images = false, have_state = false;
     bool vv32 = false;  // VV stored as float (exact: integer-valued frames)
+    bool vvp = false;   // VV stored as binary16 column pairs (vvh2_t; gqmap_math.h, policy vv_pair)
     bool lit = false;   // GQMAP_ARITH_LITERAL: k_iter_lit, literal table layout
     int split = 1;      // lanes per node of the arithmetic (Q): 1, 2, 4, 8, 16, 64
     int kq = 1;         // kernel shape: split, or 0 = role split (Q = 1 arithmetic, 16 x 8 tiles)
@@ -2445,7 +2447,7 @@ bool state_nt(const gqmap_ctx *c)
 bool band_rows(const gqmap_ctx *c)
 {
     if (c->pol.band_rows >= 0) return c->pol.band_rows == 1;
-    const size_t vsz = c->fp32 ? sizeof(float) : c->vv32 ? sizeof(vvs_t) : sizeof(double);
+    const size_t vsz = c->fp32 ? sizeof(float) : c->vvp ? sizeof(vvh2_t) : c->vv32 ? sizeof(vvs_t) : sizeof(double);
     return vv_elems(c->Mo, c->No) * vsz > ((size_t)4 << 20);
 }
 
@@ -2557,7 +2559,7 @@ void launch_k_iter(gqmap_ctx *c, const TileSegs *sg)
     }
     // (whole grid, one block per tile; lpar_xcd interleaves components instead)
     if (!sg && !P.lpar_xcd) P.band_rows = band_rows(c) ? 1 : 0;
-    if constexpr (Q == 1 && ENG == 0 && sizeof(R) == 8) {
+    if constexpr (Q == 1 && ENG == 0 && sizeof(R) == 8 && !is_vvh2<VT>::value) {
         if (c->lit) {  // literal-order arithmetic (one instantiation per VV storage and store kind)
             static const int2 lshape = kernel_shape(k_iter_lit<VT>);
             if (P.cu_group > 1) P.cu_group = lshape.x;
@@ -2632,6 +2634,7 @@ void launch_iter(gqmap_ctx *c, const TileSegs *sg = nullptr)
 {
     c->ctl_known = false;
     if (c->fp32) launch_iter_t<float, float>(c, sg);
+    else if (c->vvp) launch_k_iter<double, vvh2_t, 0, 1>(c, sg);  // (vv_pair_ok: mixture, Q = 1)
     else if (c->vv32) launch_iter_t<double, vvs_t>(c, sg);
     else launch_iter_t<double, double>(c, sg);
 }
@@ -3368,6 +3371,7 @@ bool launch_flow(gqmap_ctx *c, int n, bool dry)
         c->comm || c->nranks != 0 || !fused_finalize(c) || n < 1)
         return false;
     if (c->fp32) return launch_flow_t<float, float>(c, n, dry);
+    if (c->vvp) return !c->lit && c->kq == 1 && launch_flow_q<double, vvh2_t, 0, 1>(c, n, dry);
     if (c->vv32) return launch_flow_t<double, vvs_t>(c, n, dry);
     return launch_flow_t<double, double>(c, n, dry);
 }
@@ -3554,7 +3558,7 @@ gqmap_status download(gqmap_ctx *c, double *dst, const void *src, size_t n)
 
 // Shape checks and (re)allocation for a Mo x No frame pair; VV storage type
 // vv32 (float) or double.  Invalidates the state when the grid changes.
-gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
+gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32, bool vvp = false)
 {
     GQ_CHECK(Mo >= 4 && No >= 4, GQMAP_ERR_INVALID_ARG, "image %dx%d too small", Mo, No);
     if (c->super_)
@@ -3565,9 +3569,18 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
     GQ_CHECK(Ng >= c->n_tiles, GQMAP_ERR_INVALID_ARG, "%d node columns cannot feed %d tiles", Ng,
              c->n_tiles);
     DeviceGuard dg(c->device);
-    const bool resize = Mo != c->Mo || No != c->No || vv32 != c->vv32 || !c->d_VV;
+    const bool geom = Mo != c->Mo || No != c->No;
     strip_geometry(c, Mo, No);
+    tile_grid(c);  // (the lanes per node of this grid; alloc_grid repeats it)
+    // the column-pair store serves the one-lane-per-node kernels only (the
+    // lanes per node follow the grid): else the float store, exact as well
+    if (vvp && (c->kq != 1 || c->split != 1)) {
+        vvp = false;
+        vv32 = true;
+    }
+    const bool resize = geom || vv32 != c->vv32 || vvp != c->vvp || !c->d_VV;
     c->vv32 = vv32;
+    c->vvp = vvp;
     if (resize) {
         drop_graph(c);
         // every buffer below may still be read by work queued on the context
@@ -3580,7 +3593,7 @@ gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32)
         if (c->d_truth) (void)hipFree(c->d_truth);
         c->d_truth = nullptr;
         c->truth_elems = 0;
-        const size_t vsz = c->fp32 ? sizeof(float) : vv32 ? sizeof(vvs_t) : sizeof(double);
+        const size_t vsz = c->fp32 ? sizeof(float) : vvp ? sizeof(vvh2_t) : vv32 ? sizeof(vvs_t) : sizeof(double);
         // zero tail past the padded frame (gqmap_math.h vv_elems, axis_cell_abs).
         // Stream-ordered: the context stream is non-blocking, so a null-stream
         // memset would be unordered with the VV upload / convert_device that
@@ -3850,11 +3863,33 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
         for (double v : VV)
             if ((double)(vvs_t)v != v) { vv32 = false; break; }
     }
-    gqmap_status s = prepare_images(c, Mo, No, vv32);
+    // binary16 column pairs (gqmap_math.h vvh2_t): the fp64 single-scale
+    // mixture engine at one lane per node on one whole grid, every value exact
+    bool vvp = vv32 && !c->fp32 && c->pol.vv_pair && !c->lit && !c->super_ &&
+               c->opt.engine == GQMAP_ENGINE_MIXTURE && c->n_tiles == 1;
+    if (vvp)
+        for (double v : VV)
+            if ((double)(float)(_Float16)v != v) { vvp = false; break; }
+    if (vvp) vv32 = false;
+    gqmap_status s = prepare_images(c, Mo, No, vv32, vvp);  // (may fall back to float: c->vvp)
     if (s != GQMAP_OK) return s;
+    vvp = c->vvp;
+    vv32 = c->vv32;
     DeviceGuard dg(c->device);
     // every copy on the context stream, after prepare_images' zero fill
-    if (vv32 && !c->fp32) {
+    if (vvp) {
+        // element (r, c): rows r of columns c and c + 1 (the column past the
+        // frame is the zero column of the buffer)
+        const size_t M2 = (size_t)Mo + 2, N2 = (size_t)No + 2;
+        std::vector<vvh2_t> vp(VV.size());
+        for (size_t cc = 0; cc < N2; ++cc)
+            for (size_t r = 0; r < M2; ++r) {
+                vp[r + M2 * cc].lo = (_Float16)VV[r + M2 * cc];
+                vp[r + M2 * cc].hi = cc + 1 < N2 ? (_Float16)VV[r + M2 * (cc + 1)] : (_Float16)0;
+            }
+        GQ_HIP(hipMemcpyAsync(c->d_VV, vp.data(), vp.size() * sizeof(vvh2_t), hipMemcpyHostToDevice, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+    } else if (vv32 && !c->fp32) {
         std::vector<vvs_t> vc(VV.size());
         for (size_t k = 0; k < VV.size(); ++k) vc[k] = (vvs_t)VV[k];
         GQ_HIP(hipMemcpyAsync(c->d_VV, vc.data(), vc.size() * sizeof(vvs_t), hipMemcpyHostToDevice, c->stream));
@@ -4288,7 +4323,7 @@ int gqmap_debug_policy(const char *name, int value)
         {"cu_group", &g_pol.cu_group, -1},   {"lpar", &g_pol.lpar, -1},
         {"lpar_xcd", &g_pol.lpar_xcd, 1},    {"fused_finalize", &g_pol.fused_finalize, 1},
         {"persist", &g_pol.persist, 1},      {"persist_cap", &g_pol.persist_cap, -1},
-        {"graph", &g_pol.graph, 1},          {"vv_float", &g_pol.vv_float, 1},
+        {"graph", &g_pol.graph, 1},          {"vv_float", &g_pol.vv_float, 1}, {"vv_pair", &g_pol.vv_pair, 1},
         {"verbose", &g_pol.verbose, 0},      {"flow", &g_pol.flow, -1},
     };
     for (const Field &f : fields)
@@ -4371,6 +4406,8 @@ gqmap_status gqmap_log_p(gqmap_ctx *c, const double *map, double *logp)
         if (c->fp32) {
             if (c->super_) k_logp<float, float, true><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
             else k_logp<float, float, false><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
+        } else if (c->vvp) {
+            k_logp<double, vvh2_t, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, vvh2_t>(c), (const double *)d_map, d_part);
         } else if (c->vv32) {
             if (c->super_) k_logp<double, vvs_t, true><<<blocks, 256, 0, c->stream>>>(iter_params<double, vvs_t>(c), (const double *)d_map, d_part);
             else k_logp<double, vvs_t, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, vvs_t>(c), (const double *)d_map, d_part);
@@ -4424,8 +4461,15 @@ gqmap_status gqmap_debug_read_vv(gqmap_ctx *c, double *out, size_t n, int *store
     const size_t nvv = (size_t)(c->Mo + 2) * (c->No + 2);
     GQ_CHECK(n >= nvv, GQMAP_ERR_INVALID_ARG, "buffer holds %zu of %zu values", n, nvv);
     DeviceGuard dg(c->device);
-    const bool f32 = c->fp32 || c->vv32;
+    const bool f32 = c->fp32 || c->vv32 || c->vvp;
     if (stored_f32) *stored_f32 = f32;
+    if (c->vvp) {  // the low half of each column pair
+        std::vector<vvh2_t> raw(nvv);
+        GQ_HIP(hipMemcpyAsync(raw.data(), c->d_VV, nvv * sizeof(vvh2_t), hipMemcpyDeviceToHost, c->stream));
+        GQ_HIP(hipStreamSynchronize(c->stream));
+        for (size_t k = 0; k < nvv; ++k) out[k] = (double)(float)raw[k].lo;
+        return GQMAP_OK;
+    }
     if (!f32) {
         GQ_HIP(hipMemcpyAsync(out, c->d_VV, nvv * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         GQ_HIP(hipStreamSynchronize(c->stream));

@@ -199,6 +199,38 @@ GQ_HD VP elem_ptr(VP VV, uint32_t elem)
     return byte_ptr(VV, elem * (uint32_t)sizeof(*VV));
 }
 
+// Paired binary16 storage of the padded frame (policy vv_pair; the fp64
+// single-scale mixture engine on frames whose padded values are all exact in
+// binary16 -- the integer frames of rgb2gray, C2's within [-510, 765]):
+// element (r, c) holds the values of columns c and c + 1 of row r, so one
+// 16-byte load returns two tap columns of a cell and a sample needs two loads
+// instead of four (the gathers' address work is what bounds the node loop
+// beside the VALU: a timing probe with half the loads ran 14% faster).  Each
+// tap converts exactly (binary16 -> float -> double): the same values, so the
+// same bits as float or double storage.
+#if defined(__HIPCC__)
+struct alignas(4) vvh2_t {
+    _Float16 lo, hi;  // columns c, c + 1
+};
+template <typename T>
+struct is_vvh2 : std::is_same<typename std::remove_cv<T>::type, vvh2_t> {};
+#else
+template <typename T>
+struct is_vvh2 : std::false_type {};
+#endif
+template <typename R, typename E>
+GQ_HD R tap_col(const E &e, int half)
+{
+#if defined(__HIPCC__)
+    if constexpr (is_vvh2<E>::value) return R((float)(half ? e.hi : e.lo));
+    else
+#endif
+    {
+        (void)half;
+        return R(e);
+    }
+}
+
 // 4 x the Keys interpolation (the reference's (sum of weighted taps)/4 before
 // the /4): callers fold the 1/4 into their next operation, e.g. the residual
 // I - v as fma(v4, -1/4, I) -- v4/4 is exact, so that is I - v bit for bit.
@@ -209,15 +241,26 @@ GQ_HD R bicubic_w4(VP VV, uint32_t o, uint32_t M2, R s0, R s1, R s2, R s3, R t0,
     // taps are converted to R exactly (VV storage: double, or float when exact)
     constexpr uint32_t E = (uint32_t)sizeof(*VV);
     const uint32_t ob = o * E, cb = M2 * E;  // byte offsets: cell, column stride
-    const auto c0 = byte_ptr(VV, ob);
-    const R v0 = fma(R(c0[3]), t3, fma(R(c0[2]), t2, fma(R(c0[1]), t1, R(c0[0]) * t0)));
-    const auto c1 = byte_ptr(VV, ob + cb);
-    const R v1 = fma(R(c1[3]), t3, fma(R(c1[2]), t2, fma(R(c1[1]), t1, R(c1[0]) * t0)));
-    const auto c2 = byte_ptr(VV, ob + 2 * cb);
-    const R v2 = fma(R(c2[3]), t3, fma(R(c2[2]), t2, fma(R(c2[1]), t1, R(c2[0]) * t0)));
-    const auto c3 = byte_ptr(VV, ob + 3 * cb);
-    const R v3 = fma(R(c3[3]), t3, fma(R(c3[2]), t2, fma(R(c3[1]), t1, R(c3[0]) * t0)));
-    return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0)));
+    if constexpr (is_vvh2<typename std::remove_reference<decltype(*VV)>::type>::value) {
+        const auto p0 = byte_ptr(VV, ob), p2 = byte_ptr(VV, ob + 2 * cb);  // columns 0, 1 / 2, 3
+        R v[4];
+        for (int c = 0; c < 4; ++c) {
+            const auto p = c < 2 ? p0 : p2;
+            const int h = c & 1;
+            v[c] = fma(tap_col<R>(p[3], h), t3, fma(tap_col<R>(p[2], h), t2, fma(tap_col<R>(p[1], h), t1, tap_col<R>(p[0], h) * t0)));
+        }
+        return fma(s3, v[3], fma(s2, v[2], fma(s1, v[1], s0 * v[0])));
+    } else {
+        const auto c0 = byte_ptr(VV, ob);
+        const R v0 = fma(R(c0[3]), t3, fma(R(c0[2]), t2, fma(R(c0[1]), t1, R(c0[0]) * t0)));
+        const auto c1 = byte_ptr(VV, ob + cb);
+        const R v1 = fma(R(c1[3]), t3, fma(R(c1[2]), t2, fma(R(c1[1]), t1, R(c1[0]) * t0)));
+        const auto c2 = byte_ptr(VV, ob + 2 * cb);
+        const R v2 = fma(R(c2[3]), t3, fma(R(c2[2]), t2, fma(R(c2[1]), t1, R(c2[0]) * t0)));
+        const auto c3 = byte_ptr(VV, ob + 3 * cb);
+        const R v3 = fma(R(c3[3]), t3, fma(R(c3[2]), t2, fma(R(c3[1]), t1, R(c3[0]) * t0)));
+        return fma(s3, v3, fma(s2, v2, fma(s1, v1, s0 * v0)));
+    }
 }
 
 // 4 x the Keys interpolation in the cell whose first tap is element o, at
@@ -245,11 +288,19 @@ GQ_HD auto load_taps16(VP VV, uint32_t o, uint32_t M2)
     constexpr uint32_t EB = (uint32_t)sizeof(E);
     const uint32_t ob = o * EB, cb = M2 * EB;
     Taps16<E> T;
-    for (int c = 0; c < 4; ++c) {
-        const auto col = byte_ptr(VV, ob + (uint32_t)c * cb);
-        for (int r = 0; r < 4; ++r) T.v[4 * c + r] = col[r];
+    if constexpr (is_vvh2<E>::value) {  // v[4 p + r]: row r of column pair p (columns 2p, 2p + 1)
+        for (int pr = 0; pr < 2; ++pr) {
+            const auto col = byte_ptr(VV, ob + (uint32_t)(2 * pr) * cb);
+            for (int r = 0; r < 4; ++r) T.v[4 * pr + r] = col[r];
+        }
+        return T;
+    } else {
+        for (int c = 0; c < 4; ++c) {
+            const auto col = byte_ptr(VV, ob + (uint32_t)c * cb);
+            for (int r = 0; r < 4; ++r) T.v[4 * c + r] = col[r];
+        }
+        return T;
     }
-    return T;
 }
 template <typename R, typename E>
 GQ_HD R bicubic_taps4(const Taps16<E> &T, R so, R to)
@@ -258,8 +309,16 @@ GQ_HD R bicubic_taps4(const Taps16<E> &T, R so, R to)
     keys4(to, t0, t1, t2, t3);
     keys4(so, s0, s1, s2, s3);
     R v[4];
-    for (int c = 0; c < 4; ++c)
-        v[c] = fma(R(T.v[4 * c + 3]), t3, fma(R(T.v[4 * c + 2]), t2, fma(R(T.v[4 * c + 1]), t1, R(T.v[4 * c]) * t0)));
+    if constexpr (is_vvh2<E>::value) {
+        for (int c = 0; c < 4; ++c) {
+            const E *p = T.v + 4 * (c >> 1);
+            const int h = c & 1;
+            v[c] = fma(tap_col<R>(p[3], h), t3, fma(tap_col<R>(p[2], h), t2, fma(tap_col<R>(p[1], h), t1, tap_col<R>(p[0], h) * t0)));
+        }
+    } else {
+        for (int c = 0; c < 4; ++c)
+            v[c] = fma(R(T.v[4 * c + 3]), t3, fma(R(T.v[4 * c + 2]), t2, fma(R(T.v[4 * c + 1]), t1, R(T.v[4 * c]) * t0)));
+    }
     return fma(s3, v[3], fma(s2, v[2], fma(s1, v[1], s0 * v[0])));
 }
 
@@ -818,7 +877,7 @@ GQ_HD Sums<R> node_sums(TP tab, int k0, int K2, int dk, const TV &V, IP I1, int 
         }
         return S;
     }
-    if (ENG != 1) {
+    if constexpr (ENG != 1) {
         const R I = I1[m + (int64_t)Mo * n];
         if constexpr (ENG == 0 && sizeof(R) == 8) {
             // fp64 single-scale: absolute positions X = j + x1 with the pixel
