@@ -165,7 +165,8 @@ def debug_policy(name: str, value: int) -> None:
     """Set one execution policy of the library (gqmap_debug_policy, not in the
     public header): placement / caching / launch-shape choices that never
     change a result -- nt_state, band_rows, cu_group, lpar, lpar_xcd,
-    fused_finalize, persist, persist_cap, graph, vv_float, verbose.  value -1
+    fused_finalize, persist, persist_cap, graph, vv_float, vv_pair, flow,
+    verbose.  value -1
     restores the automatic choice.  Contexts created afterwards use it."""
     f = load().gqmap_debug_policy
     f.restype = C.c_int
