@@ -1677,6 +1677,17 @@ __device__ __forceinline__ int flow_wait(unsigned *fl, unsigned *bar, int tiles_
             }
             __builtin_amdgcn_s_sleep(GQ_PERSIST_SLEEP);
         }
+        // The lanes read the finalized count and the stop word in the same
+        // poll, unordered: lane 6 may have read a stop word older than the
+        // count lane 5 saw.  finalize(s) stores the stop word before it
+        // publishes the count (release), so after an acquire load of the
+        // count the stop word is current: an item past a stop never runs
+        // (at lag 2 an item of iteration s + 2 would overwrite state s).
+        if (x == 0 && go && fin_need > 0) {
+            (void)__hip_atomic_load(fl + FL_FIN, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned st = __hip_atomic_load(fl + FL_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (st != 0 && (int)st - 1 < j) go = 0;
+        }
         if (x == 0) *sh = go;
     }
     __syncthreads();
@@ -2634,7 +2645,7 @@ void launch_iter(gqmap_ctx *c, const TileSegs *sg = nullptr)
 {
     c->ctl_known = false;
     if (c->fp32) launch_iter_t<float, float>(c, sg);
-    else if (c->vvp) launch_k_iter<double, vvh2_t, 0, 1>(c, sg);  // (vv_pair_ok: mixture, Q = 1)
+    else if (c->vvp) launch_k_iter<double, vvh2_t, 0, 1>(c, sg);  // (the pair store: mixture at Q = 1)
     else if (c->vv32) launch_iter_t<double, vvs_t>(c, sg);
     else launch_iter_t<double, double>(c, sg);
 }
@@ -3557,6 +3568,17 @@ gqmap_status download(gqmap_ctx *c, double *dst, const void *src, size_t n)
 
 
 // Shape checks and (re)allocation for a Mo x No frame pair; VV storage type
+// Whether the binary16 column-pair store may serve this context (its values
+// checked by the caller; prepare_images also needs one lane per node): the
+// fp64 single-scale mixture engine on one whole grid (the ctf levels
+// measured neutral with it, the literal-order engine slower:
+// profiles/r06_vvpair_ctf_ab.txt, r06_vvpair_literal_ab.txt).
+bool vv_pair_candidate(const gqmap_ctx *c)
+{
+    return !c->fp32 && c->pol.vv_pair && !c->lit && !c->super_ && c->n_tiles == 1 &&
+           c->opt.engine == GQMAP_ENGINE_MIXTURE;
+}
+
 // vv32 (float) or double.  Invalidates the state when the grid changes.
 gqmap_status prepare_images(gqmap_ctx *c, int Mo, int No, bool vv32, bool vvp = false)
 {
@@ -3631,6 +3653,8 @@ gqmap_status ctx_set_images_device(gqmap_ctx *c, const double *dI1, const double
     bool vv32 = c->fp32;
     if (!vv32 && c->pol.vv_float)
         GQ_HIP(f32_exact_device(d_scratch, nvv, d_flag, &vv32, c->stream));
+    // (the column-pair store: host frames of the single-scale mixture engine
+    // only -- on the ctf levels it measured neutral, profiles/r06_vvpair_ctf_ab.txt)
     gqmap_status s = prepare_images(c, Mo, No, vv32);
     if (s != GQMAP_OK) return s;
     GQ_HIP(convert_device(d_scratch, c->d_VV, nvv, vv32, c->stream));
@@ -3865,8 +3889,7 @@ gqmap_status gqmap_set_images(gqmap_ctx *c, const double *I1, const double *I2, 
     }
     // binary16 column pairs (gqmap_math.h vvh2_t): the fp64 single-scale
     // mixture engine at one lane per node on one whole grid, every value exact
-    bool vvp = vv32 && !c->fp32 && c->pol.vv_pair && !c->lit && !c->super_ &&
-               c->opt.engine == GQMAP_ENGINE_MIXTURE && c->n_tiles == 1;
+    bool vvp = vv32 && vv_pair_candidate(c);
     if (vvp)
         for (double v : VV)
             if ((double)(float)(_Float16)v != v) { vvp = false; break; }
