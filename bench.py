@@ -520,8 +520,8 @@ def run_engine_config(args, rank, world, local, barrier, engine, names, L, K, ex
     ksuf = {"mixture": 0, "super": 1}[engine]
     R = "double" if args.precision == "fp64" else "float"
     # the padded frame's store (integer frames): binary16 column pairs for
-    # the fp64 mixture engine at one lane per node (policy vv_pair), else float
-    pair = (engine == "mixture" and args.precision == "fp64" and split == 1 and "vv_pair=0" not in args.policy)
+    # the mixture engine at one lane per node (policy vv_pair), else float
+    pair = (engine == "mixture" and split == 1 and "vv_pair=0" not in args.policy)
     vvt = "vvh2_t" if pair else "float"
     vvs = ("VV stored as binary16 column pairs: integer frames" if pair else
            "VV stored as float: integer frames")

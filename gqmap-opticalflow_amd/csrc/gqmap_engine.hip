@@ -2644,7 +2644,10 @@ void launch_iter_t(gqmap_ctx *c, const TileSegs *sg)
 void launch_iter(gqmap_ctx *c, const TileSegs *sg = nullptr)
 {
     c->ctl_known = false;
-    if (c->fp32) launch_iter_t<float, float>(c, sg);
+    if (c->fp32) {
+        if (c->vvp) launch_k_iter<float, vvh2_t, 0, 1>(c, sg);
+        else launch_iter_t<float, float>(c, sg);
+    }
     else if (c->vvp) launch_k_iter<double, vvh2_t, 0, 1>(c, sg);  // (the pair store: mixture at Q = 1)
     else if (c->vv32) launch_iter_t<double, vvs_t>(c, sg);
     else launch_iter_t<double, double>(c, sg);
@@ -3381,7 +3384,9 @@ bool launch_flow(gqmap_ctx *c, int n, bool dry)
     if (!on || c->persist_off || (c->L != 1 && c->opt.engine != GQMAP_ENGINE_SUPER) || c->n_tiles != 1 ||
         c->comm || c->nranks != 0 || !fused_finalize(c) || n < 1)
         return false;
-    if (c->fp32) return launch_flow_t<float, float>(c, n, dry);
+    if (c->fp32)
+        return c->vvp ? !c->lit && c->kq == 1 && launch_flow_q<float, vvh2_t, 0, 1>(c, n, dry)
+                      : launch_flow_t<float, float>(c, n, dry);
     if (c->vvp) return !c->lit && c->kq == 1 && launch_flow_q<double, vvh2_t, 0, 1>(c, n, dry);
     if (c->vv32) return launch_flow_t<double, vvs_t>(c, n, dry);
     return launch_flow_t<double, double>(c, n, dry);
@@ -3570,13 +3575,12 @@ gqmap_status download(gqmap_ctx *c, double *dst, const void *src, size_t n)
 // Shape checks and (re)allocation for a Mo x No frame pair; VV storage type
 // Whether the binary16 column-pair store may serve this context (its values
 // checked by the caller; prepare_images also needs one lane per node): the
-// fp64 single-scale mixture engine on one whole grid (the ctf levels
+// single-scale mixture engine (fp64 or fp32) on one whole grid (the ctf levels
 // measured neutral with it, the literal-order engine slower:
 // profiles/r06_vvpair_ctf_ab.txt, r06_vvpair_literal_ab.txt).
 bool vv_pair_candidate(const gqmap_ctx *c)
 {
-    return !c->fp32 && c->pol.vv_pair && !c->lit && !c->super_ && c->n_tiles == 1 &&
-           c->opt.engine == GQMAP_ENGINE_MIXTURE;
+    return c->pol.vv_pair && !c->lit && !c->super_ && c->n_tiles == 1 && c->opt.engine == GQMAP_ENGINE_MIXTURE;
 }
 
 // vv32 (float) or double.  Invalidates the state when the grid changes.
@@ -4428,6 +4432,7 @@ gqmap_status gqmap_log_p(gqmap_ctx *c, const double *map, double *logp)
     if (s == GQMAP_OK) {
         if (c->fp32) {
             if (c->super_) k_logp<float, float, true><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
+            else if (c->vvp) k_logp<float, vvh2_t, false><<<blocks, 256, 0, c->stream>>>(iter_params<float, vvh2_t>(c), (const float *)d_map, d_part);
             else k_logp<float, float, false><<<blocks, 256, 0, c->stream>>>(iter_params<float, float>(c), (const float *)d_map, d_part);
         } else if (c->vvp) {
             k_logp<double, vvh2_t, false><<<blocks, 256, 0, c->stream>>>(iter_params<double, vvh2_t>(c), (const double *)d_map, d_part);

@@ -47,6 +47,7 @@ LIMITS = {
     # the default on integer frames): per launch (3 waves) and as items (2)
     "_ZN2gq6k_iterIdNS_6vvh2_tELi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE": 168,
     "_ZN2gq11k_iter_flowIdNS_6vvh2_tELi0ELi1ELb0ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE": 256,
+    "_ZN2gq6k_iterIfNS_6vvh2_tELi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE": 128,  # C2 fp32 (4 waves)
 }
 # kernels that must run without a private (scratch) segment: the C2 kernels
 # of the fast arithmetic; the literal kernel is held to 3 waves by its launch
@@ -60,6 +61,7 @@ NO_SCRATCH = (
     "_ZN2gq11k_iter_flowIdfLi0ELi1ELb1ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE",
     "_ZN2gq6k_iterIdNS_6vvh2_tELi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
     "_ZN2gq11k_iter_flowIdNS_6vvh2_tELi0ELi1ELb0ELi0EEEvNS_10IterParamsIT_T0_EEiPjiPKNS_3CtlE",
+    "_ZN2gq6k_iterIfNS_6vvh2_tELi0ELi1ELb0EEEvNS_10IterParamsIT_T0_EE",
 )
 SCRATCH_MAX = {
     "_ZN2gq10k_iter_litIfLb0EEEvNS_10IterParamsIdT_EE": 128,
